@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""Headline benchmark: erasure encode+decode GiB/s (device-resident), RS(6+3), 1 MiB stripes.
+
+BASELINE.json configs[1] (encode) + configs[2] (single-erasure decode), one MI355X per rank.
+A step = encode N stripes (k data -> m parity) + decode the same N stripes with data shard 0
+lost (k survivors -> 1 rebuilt shard), both through liblstore_ec.so's device-resident C ABI
+(lsec_encode_dev / lsec_decode_dev) on the current torch stream.  Stripes are independent,
+so ranks each own N stripes (static partition, weak scaling, no collective on the data
+path; the only collectives are the timing barrier and the max-over-ranks reduction).
+
+value = k*C*N*world / max_rank(step time) / 2^30  (data GiB/s, "N KiB stripes" = C per shard)
+
+Also reported (same JSON line):
+  roofline      encode kernel: algorithmic HBM bytes (k+m)*C*N per launch / avg launch time
+                (HIP events on the launch stream) vs 8 TB/s
+  cpu_baseline  the reference CPU path (oracle/_ref: vendor/jerasure via the plan dispatch)
+                on a bounded sample of the same workload, on this box's host cores
+  host_path     PCIe-inclusive rate of et_encode_stripes / et_decode_stripes from host memory
+Every run checks parity bit-exactly against the CPU oracle on sampled stripes.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--stripes", type=int, default=4096, help="stripes per GPU")
+    ap.add_argument("--chunk", type=int, default=1 << 20, help="bytes per shard (C)")
+    ap.add_argument("--k", type=int, default=6)
+    ap.add_argument("--m", type=int, default=3)
+    ap.add_argument("--method", default="reed_sol_van")
+    ap.add_argument("--lost", type=int, default=0, help="shard lost in the decode half")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--variant", type=str, default="0,0", help="bytewise,bitsliced kernel variants")
+    return ap.parse_args()
+
+
+def cpu_baseline(method_id, k, m, C, P, lost, budget_s):
+    """Reference CPU path (oracle/_ref) on a bounded sample: encode then decode, T threads."""
+    import oracle as O
+
+    if not O.ref_available():
+        return None
+    threads = max(1, min(16, os.cpu_count() or 1))
+    # about budget_s of work at ~1 GiB/s/thread encode for RS; scale by threads, cap memory
+    n = int(max(threads, min(512, budget_s * 0.5 * threads * (1 << 30) / (k * C) / 2)))
+    tile = np.random.default_rng(1).integers(0, 256, size=(min(n, 8), k + m, C), dtype=np.uint8)
+    buf = np.empty((n, k + m, C), dtype=np.uint8)
+    for s0 in range(0, n, tile.shape[0]):
+        buf[s0:s0 + tile.shape[0]] = tile[: n - s0]
+    import ctypes as Ct
+
+    base = buf.ctypes.data
+    ptrs = (Ct.c_void_p * (n * (k + m)))(*[base + i * C for i in range(n * (k + m))])
+    rp = O.RefPlan(method_id, k, m, 8, P)
+    rp.encode_many(ptrs, min(n, threads), C, threads)  # warm tables / pages
+    t0 = time.perf_counter()
+    rp.encode_many(ptrs, n, C, threads)
+    t_enc = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    rc = rp.decode_many(ptrs, n, C, threads, [lost])
+    t_dec = time.perf_counter() - t0
+    rp.close()
+    gib = k * C * n / 2**30
+    return {"value": round(gib / (t_enc + t_dec), 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
+            "sample": f"{n} stripes x {k}+{m} x {C} B, encode then decode(lost {lost}), {threads} pthreads, "
+                      f"vendor/jerasure via oracle/_ref",
+            "encode_gibps": round(gib / t_enc, 3), "decode_gibps": round(gib / t_dec, 3), "decode_rc": rc}
+
+
+def host_path_rate(L, plan, k, m, C, lost, nstripes):
+    """et_encode_stripes / et_decode_stripes from pageable host memory (PCIe-inclusive)."""
+    tile = np.random.default_rng(2).integers(0, 256, size=(min(nstripes, 8), k + m, C), dtype=np.uint8)
+    buf = np.empty((nstripes, k + m, C), dtype=np.uint8)
+    for s0 in range(0, nstripes, tile.shape[0]):
+        buf[s0:s0 + tile.shape[0]] = tile[: nstripes - s0]
+    plan.encode_stripes(buf[:2])
+    t0 = time.perf_counter()
+    plan.encode_stripes(buf)
+    te = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    plan.decode_stripes(buf, [lost])
+    td = time.perf_counter() - t0
+    gib = k * C * nstripes / 2**30
+    return {"encode_gibps": round(gib / te, 2), "decode_gibps": round(gib / td, 2),
+            "combined_gibps": round(gib / (te + td), 2), "stripes": nstripes,
+            "note": "pageable host buffers -> pinned staging -> H2D -> kernel -> D2H -> host"}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    import lstore_amd as L
+    from lstore_amd import erasure as E
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    bw_v, bs_v = (int(x) for x in a.variant.split(","))
+    E.set_kernel_variant(bw_v, bs_v)
+
+    method = E.JE_METHOD_NAMES.index(a.method)
+    k, m, C, N = a.k, a.m, a.chunk, a.stripes
+    plan = L.Plan.for_chunk(method, k, m, C)
+    P = plan.packet_size
+
+    # synthetic stripes, resident in HBM before timing (different per rank)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    data = torch.randint(0, 256, (N, k, C), dtype=torch.uint8, device=dev, generator=g)
+    par = torch.empty((N, m, C), dtype=torch.uint8, device=dev)
+    rebuilt = torch.empty((N, 1, C), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    enc_refs, _, _ = plan.tensor_refs(data, par)
+    enc_arr = plan.shard_refs(enc_refs)
+    dec_refs = list(enc_refs)
+    dec_refs[a.lost] = (rebuilt.data_ptr(), rebuilt.stride(0))
+    dec_arr = plan.shard_refs(dec_refs)
+    er = E._erasure_array([a.lost])
+    plan.prepare_decode([a.lost])
+    lib = E.lib()
+
+    def encode():
+        rc = lib.lsec_encode_dev(plan.ptr, enc_arr, N, C, sh)
+        if rc:
+            raise E.ErasureError(E.last_error())
+
+    def decode():
+        rc = lib.lsec_decode_dev(plan.ptr, dec_arr, N, C, er, sh)
+        if rc:
+            raise E.ErasureError(E.last_error())
+
+    for _ in range(a.warmup):
+        encode()
+        decode()
+    torch.cuda.synchronize()
+
+    # ---- timed region: K steps, barrier + synchronize on both sides
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        encode()
+        decode()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- per-kernel timing with HIP events on the launch stream (roofline)
+    reps = max(3, min(10, a.steps))
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record(stream)
+    for _ in range(reps):
+        encode()
+    ev[1].record(stream)
+    for _ in range(reps):
+        decode()
+    ev[2].record(stream)
+    torch.cuda.synchronize()
+    t_enc = ev[0].elapsed_time(ev[1]) / 1e3 / reps
+    t_dec = ev[1].elapsed_time(ev[2]) / 1e3 / reps
+
+    # ---- parity check (bit-exact vs the CPU oracle on sampled stripes)
+    import oracle as O
+
+    ok = True
+    pick = sorted({0, N // 2, N - 1})
+    hd = data[pick].cpu().numpy()
+    hp = par[pick].cpu().numpy()
+    hr = rebuilt[pick].cpu().numpy()
+    for i in range(len(pick)):
+        ref = O.encode(method, hd[i], m, P)
+        ok &= bool(np.array_equal(ref, hp[i]))
+        ok &= bool(np.array_equal(hr[i, 0], np.vstack([hd[i], hp[i]])[a.lost]))
+    if not ok:
+        print(json.dumps({"error": "parity mismatch vs oracle", "rank": rank}), flush=True)
+        sys.exit(1)
+
+    data_bytes = k * C * N
+    value = data_bytes * world * a.steps / elapsed / 2**30
+    enc_hbm = (k + m) * C * N
+    dec_hbm = (k + 1) * C * N
+    achieved = enc_hbm / t_enc
+
+    out = None
+    if rank == 0:
+        cpu = None if a.no_cpu else cpu_baseline(method, k, m, C, P, a.lost, a.cpu_seconds)
+        host = None
+        if not a.no_host_path and world == 1:
+            host = host_path_rate(L, plan, k, m, C, a.lost, max(8, min(256, (4 << 30) // ((k + m) * C))))
+        out = {
+            "metric": "erasure encode+decode GiB/s (device-resident), RS(6+3) 1 MiB stripes"
+            if (method, k, m, C) == (0, 6, 3, 1 << 20) else
+            f"erasure encode+decode GiB/s (device-resident), {a.method}({k}+{m}) {C} B chunks",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (torch.randint bytes, resident in HBM)",
+            "config": {"workload": f"{a.method}({k}+{m}) encode + decode(lost shard {a.lost}), C={C} B per shard, "
+                                   f"{N} stripes/GPU, k*C={k * C} B user data per stripe",
+                       "method": a.method, "k": k, "m": m, "chunk_bytes": C, "packet_size": P,
+                       "stripes_per_gpu": N, "lost_shard": a.lost, "parallelism": f"static stripe partition x{world}"},
+            "encode_gibps": round(data_bytes / t_enc / 2**30, 2),
+            "decode_gibps": round(data_bytes / t_dec / 2**30, 2),
+            "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
+                         "kernel": "gf8_bytewise (encode)" if plan.kernel == 1 else "gf8_bitsliced (encode)",
+                         "algorithmic_bytes_per_launch": enc_hbm, "avg_launch_ms": round(t_enc * 1e3, 4),
+                         "decode_achieved_GBps": round(dec_hbm / t_dec / 1e9, 1),
+                         "decode_frac": round(dec_hbm / t_dec / HBM_PEAK, 4)},
+            "cpu_baseline": cpu,
+            "host_path": host,
+            "parity_check": "bit-exact vs oracle on stripes %s" % pick,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    plan.close()
+
+
+if __name__ == "__main__":
+    main()

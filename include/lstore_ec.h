@@ -1,0 +1,134 @@
+/*
+ * lstore_ec.h -- C ABI of liblstore_ec.so, the MI355X (gfx950) erasure-coding engine that
+ * drops in behind LStore's erasure plan service.
+ *
+ * Part 1 is the reference interface, declaration for declaration: the plan struct layout,
+ * method ids and et_* entry points of src/lio/erasure_tools.h:28-75.  LStore's segment
+ * driver dereferences the struct's fields and function pointers directly
+ * (src/lio/segment/jerasure.c:1231-1232, :1847, :2242-2243, :245), so the layout below IS
+ * the ABI and must not change.  A binary built against the reference header links against
+ * this library unchanged (INTEGRATION.md shows the build-line change).
+ *
+ * Part 2 adds batched and device-resident entry points (prefix lsec_ / et_*_stripes) that
+ * the reference does not have; they let a caller hand over many stripes per call, which is
+ * what a GPU needs (SURVEY.md §8b "recommended extension").
+ *
+ * Errors: every call that can fail returns a status (0 = success, negative = failure) and
+ * records a message for lsec_last_error().  The two void fn-pointers inherited from the
+ * reference (encode_block) cannot return a status; on failure they print the reason to
+ * stderr and abort() -- the engine never silently skips or falls back to a CPU path.
+ */
+#ifndef LSTORE_EC_H
+#define LSTORE_EC_H
+
+#include <stdio.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ===================================================================== Part 1: reference ABI */
+
+typedef struct lio_erasure_plan_t lio_erasure_plan_t;   /* src/lio/lio/erasure_tools.h:31 */
+
+/* method ids -- src/lio/erasure_tools.h:37-45 */
+#define REED_SOL_VAN    0
+#define REED_SOL_R6_OP  1
+#define CAUCHY_ORIG     2
+#define CAUCHY_GOOD     3
+#define BLAUM_ROTH      4
+#define LIBERATION      5
+#define LIBER8TION      6
+#define RAID4           7
+#define N_JE_METHODS    8
+
+/* method names -- src/lio/erasure_tools.c:35 */
+extern const char *JE_method[N_JE_METHODS];
+
+/* src/lio/erasure_tools.h:50-65 (layout-identical) */
+struct lio_erasure_plan_t {
+    long long int strip_size;   /* size of each data strip */
+    int method;                 /* encoding/decoding method */
+    int data_strips;            /* k */
+    int parity_strips;          /* m */
+    int w;                      /* word size */
+    int packet_size;            /* bitmatrix packet size */
+    int base_unit;              /* register size in bytes */
+    int *encode_matrix;         /* m x k coding matrix (matrix / Cauchy methods) */
+    int *encode_bitmatrix;      /* (m*w) x (k*w) 0/1 bitmatrix (bitmatrix methods) */
+    int **encode_schedule;      /* smart XOR schedule, -1 terminated (bitmatrix methods) */
+    int (*form_encoding_matrix)(lio_erasure_plan_t *plan);
+    int (*form_decoding_matrix)(lio_erasure_plan_t *plan);
+    void (*encode_block)(lio_erasure_plan_t *plan, char **ptr, int block_size);
+    int (*decode_block)(lio_erasure_plan_t *plan, char **ptr, int block_size, int *erasures);
+};
+
+/* replaces nearest_prime, erasure_tools.c:50-77 */
+int nearest_prime(int w, int which);
+/* replaces et_method_type, erasure_tools.c:716-725 (case-insensitive name -> id, -1 if unknown) */
+int et_method_type(char *meth);
+/* replaces et_new_plan, erasure_tools.c:606-685 */
+lio_erasure_plan_t *et_new_plan(int method, long long int strip_size,
+                                int data_strips, int parity_strips, int w, int packet_size, int base_unit);
+/* replaces et_generate_plan, erasure_tools.c:733-908 (same w / packet-size search) */
+lio_erasure_plan_t *et_generate_plan(long long int file_size, int method,
+                                     int data_strips, int parity_strips, int w, int packet_low, int packet_high);
+/* replaces et_destroy_plan, erasure_tools.c:691-710 */
+void et_destroy_plan(lio_erasure_plan_t *plan);
+/* replace the file tools et_encode / et_decode, erasure_tools.c:339-436 / :476-600 */
+int et_encode(lio_erasure_plan_t *plan, const char *fname, long long int foffset, const char *pname,
+              long long int poffset, int buffer_size);
+int et_decode(lio_erasure_plan_t *plan, long long int fsize, const char *fname, long long int foffset,
+              const char *pname, long long int poffset, int buffer_size, int *erasures);
+
+/*
+ * Semantics of the plan's fn-pointers (unchanged from the reference):
+ *   encode_block(plan, ptr, C)   ptr[0..k) data chunks, ptr[k..k+m) parity chunks, C bytes each;
+ *                                writes only ptr[k..k+m).   (segment/jerasure.c:1847)
+ *   decode_block(plan, ptr, C, erasures)  erasures = -1 terminated ids; rebuilds only the
+ *                                erased slots; 0 on success, -1 if unrecoverable.  (:245)
+ * ptr may hold host pointers (staged over PCIe) or device pointers (used in place).
+ * C must be a multiple of 8 (matrix methods) or of w*packet_size (bitmatrix methods).
+ */
+
+/* ===================================================================== Part 2: extensions */
+
+#define LSEC_ABI_VERSION 1
+
+/* Stripe-batched host-memory calls.  ptrs holds nstripes*(k+m) pointers laid out exactly
+ * like segjerase_write_func's ptr[] array (segment/jerasure.c:1647, :1812-1836): stripe s
+ * uses ptrs[s*(k+m) .. s*(k+m)+k+m).  One erasure pattern for all stripes. */
+int et_encode_stripes(lio_erasure_plan_t *plan, char **ptrs, int nstripes, int block_size);
+int et_decode_stripes(lio_erasure_plan_t *plan, char **ptrs, int nstripes, int block_size, int *erasures);
+
+/* Device-resident calls.  Shard i (0..k+m-1) of stripe s lives at
+ *   (char *)shards[i].base + s * shards[i].stride        (device memory)
+ * e.g. LStore's layout: data base = page + i*C, stride = k*C; parity base = par + i*C,
+ * stride = m*C.  Work is enqueued on `stream` (a hipStream_t; NULL = legacy default stream)
+ * and the call returns without synchronising. */
+typedef struct {
+    void *base;
+    long long stride;
+} lsec_shard_t;
+
+int lsec_encode_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int nstripes,
+                    long long block_size, void *stream);
+int lsec_decode_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int nstripes,
+                    long long block_size, const int *erasures, void *stream);
+
+/* Pre-build (and cache on the current device) the decode matrix for one erasure pattern,
+ * so the first lsec_decode_dev of that pattern does no host work.  0 / -1. */
+int lsec_prepare_decode(lio_erasure_plan_t *plan, const int *erasures);
+
+/* Engine information / control */
+int lsec_abi_version(void);
+int lsec_device_count(void);                 /* visible HIP devices, 0 if none */
+const char *lsec_last_error(void);           /* thread-local message of the last failure */
+int lsec_plan_kernel(lio_erasure_plan_t *plan); /* 1 = bytewise (matrix), 2 = bitsliced (Cauchy), 0 = none */
+void lsec_set_kernel_variant(int bytewise_variant, int bitsliced_variant);  /* tuning experiments */
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LSTORE_EC_H */

@@ -1,0 +1,1001 @@
+// ec_engine.cpp -- the C ABI of liblstore_ec.so (include/lstore_ec.h).
+//
+// Layers:
+//   plan service     et_* entry points and the plan struct's fn-pointers, with the same
+//                    arguments, return codes and struct contents as src/lio/erasure_tools.c
+//   matrix images    per (plan, device) coefficient cells for the encode matrix and, per
+//                    erasure pattern, for the decode matrix (built once, cached)
+//   submission       device-resident calls enqueue one kernel per <=8 output shards on the
+//                    caller's stream; host-memory calls go through a pooled, double-buffered
+//                    pinned staging pipeline (pack -> H2D -> kernel -> D2H -> unpack)
+//
+// There is no CPU compute path: every byte of parity or recovered data is produced by the
+// HIP kernels in ec_kernels.hip.  If the GPU is unavailable the calls fail (status -1, or
+// abort() from the void encode_block fn-pointer).
+#include <hip/hip_runtime.h>
+#include <strings.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/lstore_ec.h"
+#include "ec_kernels.h"
+#include "gf8.h"
+
+using lsec::CoefCell;
+using lsec::ShardRef;
+
+extern "C" const char *JE_method[N_JE_METHODS] = {"reed_sol_van", "reed_sol_r6_op", "cauchy_orig", "cauchy_good",
+                                                  "blaum_roth",   "liberation",     "liber8tion",  "raid4"};
+
+namespace {
+
+thread_local std::string tl_err;
+
+int fail(const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  tl_err = buf;
+  return -1;
+}
+
+#define HIP_OK(expr)                                                                             \
+  do {                                                                                           \
+    hipError_t e_ = (expr);                                                                      \
+    if (e_ != hipSuccess) return fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+
+enum KernelKind { KNONE = 0, KBYTEWISE = 1, KBITSLICED = 2 };
+
+struct DecodeEntry {
+  lsec::gf8::DecodePlan dp;
+  std::map<int, CoefCell *> dev_cells;  // device -> e x k cells
+};
+
+struct PlanImpl {
+  std::mutex mu;
+  lsec::gf8::Mat coding;   // GF(2^8) matrix the kernels apply (m x k)
+  bool coding_ready = false;
+  std::map<int, CoefCell *> enc_cells;                   // device -> m x k cells
+  std::map<std::vector<int>, DecodeEntry> decode_cache;  // sorted erased ids -> entry
+};
+
+// The public struct must stay first: callers only ever see &PlanExt::pub, and
+// et_destroy_plan / the fn-pointers recover the extension from it.
+struct PlanExt {
+  lio_erasure_plan_t pub;
+  uint64_t magic;
+  PlanImpl *impl;
+};
+constexpr uint64_t kPlanMagic = 0x4C53454350414E31ull;  // "LSECPAN1"
+
+PlanExt *ext_of(lio_erasure_plan_t *p) {
+  if (!p) return nullptr;
+  PlanExt *e = reinterpret_cast<PlanExt *>(p);
+  return e->magic == kPlanMagic ? e : nullptr;
+}
+
+int kernel_kind(int method, int w) {
+  if (w != 8) return KNONE;
+  switch (method) {
+    case REED_SOL_VAN:
+    case REED_SOL_R6_OP:
+    case RAID4:
+      return KBYTEWISE;
+    case CAUCHY_ORIG:
+    case CAUCHY_GOOD:
+      return KBITSLICED;
+    default:
+      return KNONE;  // liberation family: bitmatrix-only codes (not GF-linear per byte)
+  }
+}
+
+int *to_int_array(const lsec::gf8::Mat &m) {
+  int *a = static_cast<int *>(malloc(sizeof(int) * m.size()));
+  for (size_t i = 0; i < m.size(); ++i) a[i] = m[i];
+  return a;
+}
+
+int *to_int_array(const std::vector<int> &v) {
+  int *a = static_cast<int *>(malloc(sizeof(int) * v.size()));
+  std::memcpy(a, v.data(), sizeof(int) * v.size());
+  return a;
+}
+
+int **schedule_array(const std::vector<std::array<int, 5>> &ops) {
+  int **s = static_cast<int **>(malloc(sizeof(int *) * (ops.size() + 1)));
+  for (size_t i = 0; i < ops.size(); ++i) {
+    s[i] = static_cast<int *>(malloc(sizeof(int) * 5));
+    std::memcpy(s[i], ops[i].data(), sizeof(int) * 5);
+  }
+  s[ops.size()] = static_cast<int *>(malloc(sizeof(int) * 5));
+  s[ops.size()][0] = -1;
+  return s;
+}
+
+// Builds the plan's public matrix objects (what erasure_tools.c's form_* routines build,
+// erasure_tools.c:101-292) and the kernel's GF matrix.  `with_schedule` distinguishes
+// form_encoding_matrix (matrix + bitmatrix + schedule) from form_decoding_matrix.
+int form_matrices(lio_erasure_plan_t *p, bool with_schedule) {
+  PlanExt *e = ext_of(p);
+  if (!e) return -1;
+  std::lock_guard<std::mutex> lk(e->impl->mu);
+  const int k = p->data_strips, m = p->parity_strips, w = p->w;
+  lsec::gf8::Mat mat;
+  switch (p->method) {
+    case RAID4:
+      e->impl->coding.assign(k, 1);
+      e->impl->coding_ready = true;
+      return 0;
+    case REED_SOL_VAN:
+    case REED_SOL_R6_OP: {
+      if (!p->encode_matrix) {
+        const bool ok = (w == 8) && (p->method == REED_SOL_VAN ? lsec::gf8::reed_sol_vandermonde(k, m, mat)
+                                                               : lsec::gf8::reed_sol_r6(k, mat));
+        if (!ok) return fail("cannot form %s matrix for k=%d m=%d w=%d", JE_method[p->method], k, m, w);
+        p->encode_matrix = to_int_array(mat);
+      }
+      break;
+    }
+    case CAUCHY_ORIG:
+    case CAUCHY_GOOD: {
+      if (!p->encode_matrix) {
+        const bool ok = (w == 8) && (p->method == CAUCHY_ORIG ? lsec::gf8::cauchy_original(k, m, mat)
+                                                              : lsec::gf8::cauchy_good(k, m, mat));
+        if (!ok) return fail("cannot form %s matrix for k=%d m=%d w=%d", JE_method[p->method], k, m, w);
+        p->encode_matrix = to_int_array(mat);
+        p->encode_bitmatrix = to_int_array(lsec::gf8::to_bitmatrix(k, m, mat));
+      }
+      if (with_schedule && !p->encode_schedule) {
+        std::vector<int> bm(p->encode_bitmatrix, p->encode_bitmatrix + static_cast<size_t>(k) * m * w * w);
+        p->encode_schedule = schedule_array(lsec::gf8::smart_schedule(k, m, w, bm));
+      }
+      break;
+    }
+    case BLAUM_ROTH:
+    case LIBERATION:
+    case LIBER8TION: {
+      if (!p->encode_bitmatrix) {
+        std::vector<int> bm = p->method == LIBERATION   ? lsec::gf8::liberation_bitmatrix(k, w)
+                              : p->method == BLAUM_ROTH ? lsec::gf8::blaum_roth_bitmatrix(k, w)
+                                                        : lsec::gf8::liber8tion_bitmatrix(k);
+        if (bm.empty()) return fail("cannot form %s bitmatrix for k=%d w=%d", JE_method[p->method], k, w);
+        p->encode_bitmatrix = to_int_array(bm);
+      }
+      if (with_schedule && !p->encode_schedule) {
+        std::vector<int> bm(p->encode_bitmatrix, p->encode_bitmatrix + static_cast<size_t>(k) * m * w * w);
+        p->encode_schedule = schedule_array(lsec::gf8::smart_schedule(k, m, w, bm));
+      }
+      break;
+    }
+    default:
+      return fail("invalid method %d", p->method);
+  }
+  if (p->encode_matrix && !e->impl->coding_ready) {
+    const int rows = (p->method == REED_SOL_R6_OP) ? 2 : m;
+    e->impl->coding.resize(static_cast<size_t>(rows) * k);
+    for (size_t i = 0; i < e->impl->coding.size(); ++i) e->impl->coding[i] = static_cast<uint8_t>(p->encode_matrix[i]);
+    e->impl->coding_ready = true;
+  }
+  return 0;
+}
+
+// fn-pointer versions, with the reference's return-code behaviour
+int fp_form_encoding(lio_erasure_plan_t *p) {
+  if (!p) return -1;
+  return form_matrices(p, true);
+}
+
+int fp_form_decoding(lio_erasure_plan_t *p) {
+  if (!p) return -1;
+  const int rc = form_matrices(p, false);
+  if (rc) return rc;
+  // cauchy_*_form_coding_matrix / liberation family return -1 while the schedule is
+  // still unset (erasure_tools.c:142, :159, :176, :190, :204)
+  if (p->method != REED_SOL_VAN && p->method != REED_SOL_R6_OP && p->method != RAID4 && !p->encode_schedule)
+    return -1;
+  return 0;
+}
+
+int ensure_coding(PlanExt *e) {
+  {
+    std::lock_guard<std::mutex> lk(e->impl->mu);
+    if (e->impl->coding_ready) return 0;
+  }
+  return form_matrices(&e->pub, true);
+}
+
+void host_cells(const lsec::gf8::Mat &mat, int rows, int cols, std::vector<CoefCell> &cells) {
+  cells.resize(static_cast<size_t>(rows) * cols);
+  for (int i = 0; i < rows * cols; ++i) lsec::make_cell(mat[i], cells[i]);
+}
+
+int upload_cells(const std::vector<CoefCell> &h, CoefCell **out) {
+  CoefCell *d = nullptr;
+  HIP_OK(hipMalloc(&d, sizeof(CoefCell) * h.size()));
+  hipError_t err = hipMemcpy(d, h.data(), sizeof(CoefCell) * h.size(), hipMemcpyHostToDevice);
+  if (err != hipSuccess) {
+    (void)hipFree(d);
+    return fail("hipMemcpy(cells): %s", hipGetErrorString(err));
+  }
+  *out = d;
+  return 0;
+}
+
+// encode matrix cells on the current device
+int encode_cells(PlanExt *e, CoefCell **out) {
+  if (ensure_coding(e)) return -1;
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(e->impl->mu);
+  auto it = e->impl->enc_cells.find(dev);
+  if (it != e->impl->enc_cells.end()) {
+    *out = it->second;
+    return 0;
+  }
+  const int k = e->pub.data_strips;
+  const int rows = static_cast<int>(e->impl->coding.size()) / k;
+  std::vector<CoefCell> h;
+  host_cells(e->impl->coding, rows, k, h);
+  CoefCell *d = nullptr;
+  if (upload_cells(h, &d)) return -1;
+  e->impl->enc_cells[dev] = d;
+  *out = d;
+  return 0;
+}
+
+// Parses a -1 terminated erasure list.  Returns 0 with the sorted distinct ids, 1 if the
+// list is empty (nothing to do), -1 if unrecoverable / invalid.
+int parse_erasures(const lio_erasure_plan_t *p, const int *erasures, std::vector<int> &ids) {
+  const int k = p->data_strips, m = p->parity_strips;
+  ids.clear();
+  if (!erasures) return fail("erasures is NULL");
+  int listed = 0;
+  for (int i = 0; erasures[i] != -1; ++i) {
+    const int x = erasures[i];
+    if (x < 0 || x >= k + m) return fail("erasure id %d out of range 0..%d", x, k + m - 1);
+    ++listed;
+    if (std::find(ids.begin(), ids.end(), x) == ids.end()) ids.push_back(x);
+    if (listed > 4 * (k + m)) return fail("erasure list not terminated");
+  }
+  std::sort(ids.begin(), ids.end());
+  if (p->method == RAID4 && listed > 1) return fail("raid4 recovers one device (raid4.c:47)");
+  if (static_cast<int>(ids.size()) > m) return fail("%zu erasures exceed m=%d", ids.size(), m);
+  if (ids.empty()) return 1;
+  return 0;
+}
+
+// decode entry (host plan + device cells on the current device)
+int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, CoefCell **cells) {
+  if (ensure_coding(e)) return -1;
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(e->impl->mu);
+  auto it = e->impl->decode_cache.find(ids);
+  if (it == e->impl->decode_cache.end()) {
+    DecodeEntry ent;
+    const int k = e->pub.data_strips;
+    const int m = static_cast<int>(e->impl->coding.size()) / k;
+    if (!lsec::gf8::make_decode(k, m, e->impl->coding, ids, ent.dp)) return fail("decoding matrix is singular");
+    it = e->impl->decode_cache.emplace(ids, std::move(ent)).first;
+  }
+  DecodeEntry &ent = it->second;
+  auto dc = ent.dev_cells.find(dev);
+  if (dc == ent.dev_cells.end()) {
+    std::vector<CoefCell> h;
+    host_cells(ent.dp.rows, static_cast<int>(ent.dp.erased.size()), e->pub.data_strips, h);
+    CoefCell *d = nullptr;
+    if (upload_cells(h, &d)) return -1;
+    dc = ent.dev_cells.emplace(dev, d).first;
+  }
+  *out = &ent;
+  *cells = dc->second;
+  return 0;
+}
+
+int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
+  const int k = p->data_strips, m = p->parity_strips;
+  if (k < 1 || k > lsec::kMaxK) return fail("k=%d outside 1..%d", k, lsec::kMaxK);
+  if (m < 1) return fail("m=%d", m);
+  if (block_size < 0 || block_size % 8 != 0) return fail("block_size %lld is not a multiple of 8", block_size);
+  const int kind = kernel_kind(p->method, p->w);
+  if (kind == KNONE)
+    return fail("method %s (w=%d) has no GPU kernel in this build", JE_method[p->method], p->w);
+  if (kind == KBITSLICED) {
+    const long long sp = 8LL * p->packet_size;
+    if (p->packet_size <= 0 || p->packet_size % 4 != 0 || block_size % sp != 0)
+      return fail("block_size %lld is not a multiple of w*packet_size = %lld", block_size, sp);
+  }
+  return 0;
+}
+
+// Enqueue out[r] = rows[r] . in  for every stripe, splitting R into launches of <= 8 rows.
+int enqueue_apply(int kind, const CoefCell *cells, int K, int R, const ShardRef *in, const ShardRef *out,
+                  int nstripes, long long size, int packet, hipStream_t st) {
+  for (int r0 = 0; r0 < R; r0 += 8) {
+    lsec::ApplyArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.K = K;
+    a.R = std::min(8, R - r0);
+    a.cells = cells + static_cast<size_t>(r0) * K;
+    a.nstripes = nstripes;
+    a.size = size;
+    a.packet = packet;
+    for (int j = 0; j < K; ++j) a.in[j] = in[j];
+    for (int r = 0; r < a.R; ++r) a.out[r] = out[r0 + r];
+    // split very large batches so tile indices stay 32-bit
+    const long long per = std::max(1LL, (1LL << 30) / std::max(1LL, size / 4096 + 1));
+    for (int s0 = 0; s0 < nstripes; s0 += static_cast<int>(std::min<long long>(per, nstripes))) {
+      lsec::ApplyArgs b = a;
+      b.nstripes = static_cast<int>(std::min<long long>(per, nstripes - s0));
+      for (int j = 0; j < K; ++j) b.in[j].base = in[j].base + static_cast<uint64_t>(s0) * in[j].stride;
+      for (int r = 0; r < b.R; ++r) b.out[r].base = out[r0 + r].base + static_cast<uint64_t>(s0) * out[r0 + r].stride;
+      const hipError_t err = kind == KBYTEWISE ? lsec::launch_bytewise(b, st) : lsec::launch_bitsliced(b, st);
+      if (err != hipSuccess) return fail("kernel launch failed: %s", hipGetErrorString(err));
+    }
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------- device-resident core
+int encode_dev(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C, hipStream_t st) {
+  lio_erasure_plan_t *p = &e->pub;
+  if (check_geometry(p, C)) return -1;
+  if (nstripes <= 0 || C == 0) return 0;
+  CoefCell *cells = nullptr;
+  if (encode_cells(e, &cells)) return -1;
+  const int k = p->data_strips;
+  const int R = static_cast<int>(e->impl->coding.size()) / k;  // m (2 for r6, 1 for raid4)
+  ShardRef in[lsec::kMaxK], out[64];
+  if (R > 64) return fail("m=%d too large", R);
+  for (int j = 0; j < k; ++j) in[j] = {reinterpret_cast<uint64_t>(sh[j].base), sh[j].stride};
+  for (int r = 0; r < R; ++r) out[r] = {reinterpret_cast<uint64_t>(sh[k + r].base), sh[k + r].stride};
+  return enqueue_apply(kernel_kind(p->method, p->w), cells, k, R, in, out, nstripes, C, p->packet_size, st);
+}
+
+// returns 0 (done or nothing to do) / -1
+int decode_dev(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C, const int *erasures,
+               hipStream_t st) {
+  lio_erasure_plan_t *p = &e->pub;
+  std::vector<int> ids;
+  const int pr = parse_erasures(p, erasures, ids);
+  if (pr < 0) return -1;
+  if (pr == 1) return 0;
+  if (check_geometry(p, C)) return -1;
+  if (p->method == RAID4 && ids[0] >= p->data_strips) return 0;  // raid4.c:48 leaves lost parity alone
+  if (nstripes <= 0 || C == 0) return 0;
+  DecodeEntry *ent = nullptr;
+  CoefCell *cells = nullptr;
+  if (decode_entry(e, ids, &ent, &cells)) return -1;
+  const int k = p->data_strips;
+  ShardRef in[lsec::kMaxK], out[64];
+  for (int j = 0; j < k; ++j) {
+    const lsec_shard_t &s = sh[ent->dp.survivors[j]];
+    in[j] = {reinterpret_cast<uint64_t>(s.base), s.stride};
+  }
+  const int R = static_cast<int>(ent->dp.erased.size());
+  for (int r = 0; r < R; ++r) {
+    const lsec_shard_t &s = sh[ent->dp.erased[r]];
+    out[r] = {reinterpret_cast<uint64_t>(s.base), s.stride};
+  }
+  return enqueue_apply(kernel_kind(p->method, p->w), cells, k, R, in, out, nstripes, C, p->packet_size, st);
+}
+
+// ---------------------------------------------------------------- host staging pool
+struct Staging {
+  int dev = -1;
+  hipStream_t stream = nullptr;
+  struct Slot {
+    char *d = nullptr;   // device: [nb][nin][C] then [nb][nout][C]
+    char *h = nullptr;   // pinned host, same layout
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+    bool pending = false;
+    // what to unpack when `done` fires
+    char **ptrs = nullptr;
+    int s0 = 0, nb = 0;
+  } slot[2];
+  ~Staging() {
+    for (auto &s : slot) {
+      if (s.d) (void)hipFree(s.d);
+      if (s.h) (void)hipHostFree(s.h);
+      if (s.done) (void)hipEventDestroy(s.done);
+    }
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+std::mutex g_pool_mu;
+std::map<int, std::vector<Staging *>> g_pool;
+
+Staging *acquire_staging(int dev) {
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto &v = g_pool[dev];
+    if (!v.empty()) {
+      Staging *s = v.back();
+      v.pop_back();
+      return s;
+    }
+  }
+  Staging *s = new Staging();
+  s->dev = dev;
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete s;
+    return nullptr;
+  }
+  for (auto &sl : s->slot)
+    if (hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
+      delete s;
+      return nullptr;
+    }
+  return s;
+}
+
+void release_staging(Staging *s) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  g_pool[s->dev].push_back(s);
+}
+
+int ensure_slot(Staging::Slot &sl, size_t bytes) {
+  if (sl.cap >= bytes) return 0;
+  if (sl.d) (void)hipFree(sl.d);
+  if (sl.h) (void)hipHostFree(sl.h);
+  sl.d = nullptr;
+  sl.h = nullptr;
+  sl.cap = 0;
+  HIP_OK(hipMalloc(&sl.d, bytes));
+  HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&sl.h), bytes, hipHostMallocDefault));
+  sl.cap = bytes;
+  return 0;
+}
+
+size_t staging_budget() {
+  static size_t b = [] {
+    const char *s = getenv("LSEC_STAGING_MB");
+    const long v = s ? atol(s) : 64;
+    return static_cast<size_t>(std::max(1L, v)) << 20;
+  }();
+  return b;
+}
+
+// Shared driver of the host-memory paths.  For each stripe, `in_ids` name the shards that
+// go to the GPU and `out_ids` the shards that come back (encode: data -> parity; decode:
+// survivors -> erased).  The kernel runs on the packed staging layout.
+int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
+             const std::vector<int> &out_ids, const CoefCell *cells, int kind) {
+  lio_erasure_plan_t *p = &e->pub;
+  const int km = p->data_strips + p->parity_strips;
+  const int nin = static_cast<int>(in_ids.size()), nout = static_cast<int>(out_ids.size());
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  Staging *stg = acquire_staging(dev);
+  if (!stg) return fail("cannot create staging stream");
+  const size_t per_stripe = static_cast<size_t>(nin + nout) * C;
+  const int nb_max = static_cast<int>(std::max<size_t>(1, std::min<size_t>(nstripes, staging_budget() / std::max<size_t>(per_stripe, 1))));
+  int rc = 0;
+
+  auto unpack = [&](Staging::Slot &sl) -> int {
+    if (!sl.pending) return 0;
+    if (hipEventSynchronize(sl.done) != hipSuccess) return fail("staging event sync failed");
+    const char *outb = sl.h + static_cast<size_t>(sl.nb) * nin * C;
+    for (int s = 0; s < sl.nb; ++s)
+      for (int r = 0; r < nout; ++r)
+        std::memcpy(sl.ptrs[static_cast<size_t>(sl.s0 + s) * km + out_ids[r]], outb + (static_cast<size_t>(s) * nout + r) * C, C);
+    sl.pending = false;
+    return 0;
+  };
+
+  int which = 0;
+  for (int s0 = 0; s0 < nstripes && rc == 0; s0 += nb_max, which ^= 1) {
+    const int nb = std::min(nb_max, nstripes - s0);
+    Staging::Slot &sl = stg->slot[which];
+    if ((rc = unpack(sl))) break;
+    if ((rc = ensure_slot(sl, per_stripe * nb_max))) break;
+    // pack inputs
+    for (int s = 0; s < nb; ++s)
+      for (int j = 0; j < nin; ++j)
+        std::memcpy(sl.h + (static_cast<size_t>(s) * nin + j) * C, ptrs[static_cast<size_t>(s0 + s) * km + in_ids[j]], C);
+    const size_t in_bytes = static_cast<size_t>(nb) * nin * C;
+    const size_t out_off = static_cast<size_t>(nb) * nin * C;
+    hipError_t err = hipMemcpyAsync(sl.d, sl.h, in_bytes, hipMemcpyHostToDevice, stg->stream);
+    if (err != hipSuccess) { rc = fail("H2D: %s", hipGetErrorString(err)); break; }
+    ShardRef in[lsec::kMaxK], out[64];
+    for (int j = 0; j < nin; ++j) in[j] = {reinterpret_cast<uint64_t>(sl.d) + static_cast<uint64_t>(j) * C, static_cast<int64_t>(nin) * C};
+    for (int r = 0; r < nout; ++r)
+      out[r] = {reinterpret_cast<uint64_t>(sl.d) + out_off + static_cast<uint64_t>(r) * C, static_cast<int64_t>(nout) * C};
+    if ((rc = enqueue_apply(kind, cells, nin, nout, in, out, nb, C, p->packet_size, stg->stream))) break;
+    err = hipMemcpyAsync(sl.h + out_off, sl.d + out_off, static_cast<size_t>(nb) * nout * C, hipMemcpyDeviceToHost, stg->stream);
+    if (err != hipSuccess) { rc = fail("D2H: %s", hipGetErrorString(err)); break; }
+    err = hipEventRecord(sl.done, stg->stream);
+    if (err != hipSuccess) { rc = fail("event record: %s", hipGetErrorString(err)); break; }
+    sl.pending = true;
+    sl.ptrs = ptrs;
+    sl.s0 = s0;
+    sl.nb = nb;
+  }
+  for (auto &sl : stg->slot) {
+    const int r2 = unpack(sl);
+    if (!rc) rc = r2;
+    sl.pending = false;
+  }
+  if (rc) {
+    (void)hipStreamSynchronize(stg->stream);
+    delete stg;  // do not recycle a stream in an unknown state
+  } else {
+    release_staging(stg);
+  }
+  return rc;
+}
+
+bool is_device_ptr(const void *ptr) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, ptr) != hipSuccess) {
+    (void)hipGetLastError();  // pageable host memory reports an error on some runtimes
+    return false;
+  }
+  return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+// all k+m pointers of every stripe device memory?  then describe them as shard refs
+bool device_layout(const lio_erasure_plan_t *p, char **ptrs, int nstripes, std::vector<lsec_shard_t> &sh) {
+  const int km = p->data_strips + p->parity_strips;
+  if (!is_device_ptr(ptrs[0])) return false;
+  for (int i = 1; i < km; ++i)
+    if (!is_device_ptr(ptrs[i])) return false;
+  sh.resize(km);
+  for (int i = 0; i < km; ++i) {
+    sh[i].base = ptrs[i];
+    sh[i].stride = nstripes > 1 ? static_cast<long long>(ptrs[km + i] - ptrs[i]) : 0;
+  }
+  for (int s = 2; s < nstripes; ++s)  // require a regular stride (one layout descriptor)
+    for (int i = 0; i < km; ++i)
+      if (ptrs[static_cast<size_t>(s) * km + i] != ptrs[i] + s * sh[i].stride) return false;
+  return true;
+}
+
+hipStream_t thread_stream() {
+  // per-thread blocking stream for the synchronous fn-pointer entry points
+  static thread_local std::map<int, hipStream_t> streams;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  auto it = streams.find(dev);
+  if (it != streams.end()) return it->second;
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  streams[dev] = s;
+  return s;
+}
+
+int encode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C) {
+  lio_erasure_plan_t *p = &e->pub;
+  if (!ptrs) return fail("ptrs is NULL");
+  if (check_geometry(p, C)) return -1;
+  if (nstripes <= 0 || C == 0) return 0;
+  std::vector<lsec_shard_t> sh;
+  if (device_layout(p, ptrs, nstripes, sh)) {
+    hipStream_t st = thread_stream();
+    if (!st) return fail("no HIP stream");
+    if (encode_dev(e, sh.data(), nstripes, C, st)) return -1;
+    HIP_OK(hipStreamSynchronize(st));
+    return 0;
+  }
+  CoefCell *cells = nullptr;
+  if (encode_cells(e, &cells)) return -1;
+  const int k = p->data_strips;
+  const int R = static_cast<int>(e->impl->coding.size()) / k;
+  std::vector<int> in_ids(k), out_ids(R);
+  for (int j = 0; j < k; ++j) in_ids[j] = j;
+  for (int r = 0; r < R; ++r) out_ids[r] = k + r;
+  return run_host(e, ptrs, nstripes, C, in_ids, out_ids, cells, kernel_kind(p->method, p->w));
+}
+
+int decode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C, const int *erasures) {
+  lio_erasure_plan_t *p = &e->pub;
+  if (!ptrs) return fail("ptrs is NULL");
+  std::vector<int> ids;
+  const int pr = parse_erasures(p, erasures, ids);
+  if (pr < 0) return -1;
+  if (pr == 1) return 0;
+  if (check_geometry(p, C)) return -1;
+  if (p->method == RAID4 && ids[0] >= p->data_strips) return 0;
+  if (nstripes <= 0 || C == 0) return 0;
+  std::vector<lsec_shard_t> sh;
+  if (device_layout(p, ptrs, nstripes, sh)) {
+    hipStream_t st = thread_stream();
+    if (!st) return fail("no HIP stream");
+    if (decode_dev(e, sh.data(), nstripes, C, erasures, st)) return -1;
+    HIP_OK(hipStreamSynchronize(st));
+    return 0;
+  }
+  DecodeEntry *ent = nullptr;
+  CoefCell *cells = nullptr;
+  if (decode_entry(e, ids, &ent, &cells)) return -1;
+  return run_host(e, ptrs, nstripes, C, ent->dp.survivors, ent->dp.erased, cells, kernel_kind(p->method, p->w));
+}
+
+// plan->encode_block / plan->decode_block
+void fp_encode_block(lio_erasure_plan_t *p, char **ptr, int block_size) {
+  PlanExt *e = ext_of(p);
+  if (!e) {
+    fprintf(stderr, "lstore_ec: encode_block on a plan not created by this library\n");
+    abort();
+  }
+  if (encode_stripes_impl(e, ptr, 1, block_size) != 0) {
+    fprintf(stderr, "lstore_ec: encode_block failed: %s\n", tl_err.c_str());
+    abort();
+  }
+}
+
+int fp_decode_block(lio_erasure_plan_t *p, char **ptr, int block_size, int *erasures) {
+  PlanExt *e = ext_of(p);
+  if (!e) return fail("not an lstore_ec plan");
+  return decode_stripes_impl(e, ptr, 1, block_size, erasures);
+}
+
+int fp_dummy(lio_erasure_plan_t *) { return 0; }
+
+}  // namespace
+
+namespace lsec {
+
+void make_cell(uint8_t c, CoefCell &cell) {
+  uint8_t ta[8], tb[8], tc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int n = 0; n < 8; ++n) {
+    ta[n] = gf8::mul(c, static_cast<uint8_t>(n));
+    tb[n] = gf8::mul(c, static_cast<uint8_t>(n << 3));
+    if (n < 4) tc[n] = gf8::mul(c, static_cast<uint8_t>(n << 6));
+  }
+  auto pack = [](const uint8_t *b) {
+    return static_cast<uint32_t>(b[0]) | (static_cast<uint32_t>(b[1]) << 8) | (static_cast<uint32_t>(b[2]) << 16) |
+           (static_cast<uint32_t>(b[3]) << 24);
+  };
+  cell.coef = c;
+  cell.pad = 0;
+  cell.ta_lo = pack(ta);
+  cell.ta_hi = pack(ta + 4);
+  cell.tb_lo = pack(tb);
+  cell.tb_hi = pack(tb + 4);
+  cell.tc_lo = pack(tc);
+  cell.tc_hi = pack(tc + 4);
+}
+
+}  // namespace lsec
+
+// ==================================================================== C ABI
+extern "C" {
+
+int nearest_prime(int w, int which) {
+  static const int primes[55] = {2,   3,   5,   7,   11,  13,  17,  19,  23,  29,  31,  37,  41,  43,
+                                 47,  53,  59,  61,  67,  71,  73,  79,  83,  89,  97,  101, 103, 107,
+                                 109, 113, 127, 131, 137, 139, 149, 151, 157, 163, 167, 173, 179, 181,
+                                 191, 193, 197, 199, 211, 223, 227, 229, 233, 239, 241, 251, 257};
+  // first prime >= w among primes[1..54]; which>0 -> it, which<0 -> the one below,
+  // which==0 -> the closer of the two (ties go up)  (erasure_tools.c:50-77)
+  for (int i = 1; i < 55; ++i) {
+    if (w > primes[i]) continue;
+    if (which > 0) return primes[i];
+    if (which < 0) return primes[i - 1];
+    return (w - primes[i - 1] < primes[i] - w) ? primes[i - 1] : primes[i];
+  }
+  return primes[54];
+}
+
+int et_method_type(char *meth) {
+  if (!meth) return -1;
+  for (int i = 0; i < N_JE_METHODS; ++i)
+    if (strcasecmp(meth, JE_method[i]) == 0) return i;
+  return -1;
+}
+
+lio_erasure_plan_t *et_new_plan(int method, long long int strip_size, int data_strips, int parity_strips, int w,
+                                int packet_size, int base_unit) {
+  if (method < 0 || method >= N_JE_METHODS) {
+    fail("et_new_plan: invalid method %d", method);
+    return nullptr;
+  }
+  PlanExt *e = static_cast<PlanExt *>(calloc(1, sizeof(PlanExt)));
+  if (!e) return nullptr;
+  e->magic = kPlanMagic;
+  e->impl = new PlanImpl();
+  lio_erasure_plan_t *p = &e->pub;
+  p->method = method;
+  p->strip_size = strip_size;
+  p->data_strips = data_strips;
+  p->parity_strips = parity_strips;
+  p->w = w;
+  p->base_unit = base_unit;
+  p->packet_size = packet_size;
+  if (method == RAID4) {
+    p->form_encoding_matrix = fp_dummy;
+    p->form_decoding_matrix = fp_dummy;
+  } else {
+    p->form_encoding_matrix = fp_form_encoding;
+    p->form_decoding_matrix = fp_form_decoding;
+  }
+  p->encode_block = fp_encode_block;
+  p->decode_block = fp_decode_block;
+  return p;
+}
+
+void et_destroy_plan(lio_erasure_plan_t *p) {
+  if (!p) return;
+  PlanExt *e = ext_of(p);
+  free(p->encode_matrix);
+  free(p->encode_bitmatrix);
+  if (p->encode_schedule) {
+    int i = 0;
+    for (; p->encode_schedule[i][0] != -1; ++i) free(p->encode_schedule[i]);
+    free(p->encode_schedule[i]);
+    free(p->encode_schedule);
+  }
+  if (e) {
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    for (auto &kv : e->impl->enc_cells) {
+      (void)hipSetDevice(kv.first);
+      (void)hipFree(kv.second);
+    }
+    for (auto &ent : e->impl->decode_cache)
+      for (auto &kv : ent.second.dev_cells) {
+        (void)hipSetDevice(kv.first);
+        (void)hipFree(kv.second);
+      }
+    if (cur >= 0) (void)hipSetDevice(cur);
+    delete e->impl;
+    e->magic = 0;
+  }
+  free(e ? static_cast<void *>(e) : static_cast<void *>(p));
+}
+
+lio_erasure_plan_t *et_generate_plan(long long int file_size, int method, int data_strips, int parity_strips, int w,
+                                     int packet_low, int packet_high) {
+  int base_unit = 8;
+  if (w == -1) {  // auto word size (erasure_tools.c:746-776)
+    switch (method) {
+      case REED_SOL_R6_OP: case REED_SOL_VAN: case CAUCHY_ORIG: case CAUCHY_GOOD: case LIBER8TION:
+        w = 8;
+        break;
+      case BLAUM_ROTH: w = nearest_prime(data_strips + 1, 1) - 1; break;
+      case LIBERATION: w = nearest_prime(data_strips, 1); break;
+      case RAID4: w = 8; base_unit = 1; break;
+      default:
+        fail("et_generate_plan: invalid method %d", method);
+        return nullptr;
+    }
+  }
+  // search range (erasure_tools.c:779-796)
+  const long long approx = file_size / (static_cast<long long>(w) * base_unit * data_strips);
+  const int plow = approx < 4 * 1024 ? static_cast<int>(approx / 4) : 512;
+  const int phigh = approx < 4 * 1024 ? static_cast<int>(approx) : 4096;
+  if (packet_low < 0) packet_low = plow;
+  if (packet_high < 0) packet_high = phigh;
+  if (packet_low > packet_high) {
+    fail("et_generate_plan: packet_low > packet_high (%d > %d)", packet_low, packet_high);
+    return nullptr;
+  }
+  packet_low = (packet_low / base_unit) * base_unit;
+  packet_high = (packet_high / base_unit) * base_unit;
+  // validation (erasure_tools.c:801-872)
+  switch (method) {
+    case REED_SOL_R6_OP:
+      if (parity_strips != 2) { fail("%s needs parity_strips == 2", JE_method[method]); return nullptr; }
+      [[fallthrough]];
+    case REED_SOL_VAN: case CAUCHY_ORIG: case CAUCHY_GOOD:
+      if (w != 8 && w != 16 && w != 32) { fail("%s needs w in {8,16,32}", JE_method[method]); return nullptr; }
+      break;
+    case BLAUM_ROTH:
+      if (data_strips > w || nearest_prime(w + 1, 0) != w + 1 || packet_high % 8 != 0) {
+        fail("blaum_roth: need k <= w, w+1 prime, packet %% 8 == 0");
+        return nullptr;
+      }
+      break;
+    case LIBERATION:
+      if (data_strips > w || nearest_prime(w, 0) != w || packet_high % 8 != 0) {
+        fail("liberation: need k <= w, w prime, packet %% 8 == 0");
+        return nullptr;
+      }
+      break;
+    case LIBER8TION:
+      if (w != 8 || parity_strips != 2 || data_strips > w) { fail("liber8tion: need w == 8, m == 2, k <= 8"); return nullptr; }
+      break;
+    case RAID4:
+      if (parity_strips != 1) { fail("raid4 needs parity_strips == 1"); return nullptr; }
+      base_unit = 1;
+      packet_low = 0;
+      packet_high = 1;
+      break;
+    default:
+      fail("et_generate_plan: invalid method %d", method);
+      return nullptr;
+  }
+  // packet search: least padding, ties to the smaller packet, stop below 1 % (erasure_tools.c:876-896)
+  long long best_excess = 10 * file_size, best_size = 0;
+  int best_packet = -1;
+  for (int ps = packet_high; ps > packet_low; ps -= base_unit) {
+    const long long unit = static_cast<long long>(data_strips) * w * ps * base_unit;
+    long long size = file_size;
+    const long long rem = size % unit;
+    if (rem > 0) size += unit - rem;
+    const int excess = static_cast<int>(size - file_size);
+    if (excess <= best_excess) {
+      best_excess = excess;
+      best_packet = ps;
+      best_size = size;
+      const float pct = (1.0f * excess) / file_size * 100;
+      if (pct < 1) break;
+    }
+  }
+  return et_new_plan(method, best_size / data_strips, data_strips, parity_strips, w, best_packet, base_unit);
+}
+
+// ---- file tools (erasure_tools.c:339-600): same file layout and padding ('0' bytes past EOF)
+static size_t bread(char *buf, size_t n, FILE *f) {
+  const size_t got = fread(buf, 1, n, f);
+  if (got < n) memset(buf + got, '0', n - got);  // BLANK_CHAR, erasure_tools.c:37
+  return n;
+}
+
+static int file_block(const lio_erasure_plan_t *p, int buffer_size) {
+  const int unit = (p->data_strips + p->parity_strips) * p->w * p->packet_size * p->base_unit;
+  if (unit <= 0) return -1;
+  if (buffer_size == 0) buffer_size = 10 * 1024 * 1024;
+  int j = buffer_size / unit;
+  if (j == 0) j = 1;
+  return j * unit / (p->data_strips + p->parity_strips);
+}
+
+int et_encode(lio_erasure_plan_t *plan, const char *fname, long long int foffset, const char *pname,
+              long long int poffset, int buffer_size) {
+  if (!ext_of(plan)) return fail("not an lstore_ec plan"), 1;
+  FILE *fd = fopen(fname, "r");
+  if (!fd) return fail("et_encode: cannot open %s", fname), 1;
+  FILE *fp = fopen(pname, "r+");
+  if (!fp) fp = fopen(pname, "w");
+  if (!fp) { fclose(fd); return fail("et_encode: cannot open %s", pname), 1; }
+  plan->form_encoding_matrix(plan);
+  const int k = plan->data_strips, m = plan->parity_strips;
+  const int block = file_block(plan, buffer_size);
+  std::vector<char> buf(static_cast<size_t>(block) * (k + m));
+  std::vector<char *> ptr(k + m);
+  for (int i = 0; i < k + m; ++i) ptr[i] = buf.data() + static_cast<size_t>(i) * block;
+  int rc = 0;
+  for (long long rpos = 0, apos = foffset, ppos = poffset; rpos < plan->strip_size && rc == 0;
+       rpos += block, apos += block, ppos += block) {
+    const int bsize = static_cast<int>(std::min<long long>(block, plan->strip_size - rpos));
+    for (int i = 0; i < k; ++i) {
+      fseek(fd, apos + i * plan->strip_size, SEEK_SET);
+      bread(ptr[i], bsize, fd);
+    }
+    if (encode_stripes_impl(ext_of(plan), ptr.data(), 1, bsize)) { rc = 1; break; }
+    for (int i = 0; i < m; ++i) {
+      fseek(fp, ppos + i * plan->strip_size, SEEK_SET);
+      if (fwrite(ptr[k + i], 1, bsize, fp) != static_cast<size_t>(bsize)) rc = 1;
+    }
+  }
+  fclose(fd);
+  fclose(fp);
+  return rc;
+}
+
+int et_decode(lio_erasure_plan_t *plan, long long int fsize, const char *fname, long long int foffset,
+              const char *pname, long long int poffset, int buffer_size, int *erasures) {
+  if (!ext_of(plan)) return fail("not an lstore_ec plan"), 1;
+  const int k = plan->data_strips, m = plan->parity_strips;
+  std::vector<int> missing(k + m, 0);
+  int n = 0;
+  for (; erasures[n] != -1; ++n) {
+    if (erasures[n] < 0 || erasures[n] >= k + m) return fail("erasure id out of range"), 1;
+    missing[erasures[n]] = 1;
+  }
+  if (n == 0) return 0;
+  FILE *fd = fopen(fname, "r+");
+  if (!fd) return fail("et_decode: cannot open %s", fname), 1;
+  FILE *fp = fopen(pname, "r+");
+  if (!fp) { fclose(fd); return fail("et_decode: cannot open %s", pname), 1; }
+  plan->form_decoding_matrix(plan);
+  const int block = file_block(plan, buffer_size);
+  std::vector<char> buf(static_cast<size_t>(block) * (k + m));
+  std::vector<char *> ptr(k + m);
+  for (int i = 0; i < k + m; ++i) ptr[i] = buf.data() + static_cast<size_t>(i) * block;
+  int rc = 0;
+  for (long long rpos = 0, apos = foffset, ppos = poffset; rpos < plan->strip_size && rc == 0;
+       rpos += block, apos += block, ppos += block) {
+    const int bsize = static_cast<int>(std::min<long long>(block, plan->strip_size - rpos));
+    for (int i = 0; i < k; ++i)
+      if (!missing[i]) {
+        fseek(fd, apos + i * plan->strip_size, SEEK_SET);
+        bread(ptr[i], bsize, fd);
+      }
+    for (int i = 0; i < m; ++i)
+      if (!missing[k + i]) {
+        fseek(fp, ppos + i * plan->strip_size, SEEK_SET);
+        if (fread(ptr[k + i], 1, bsize, fp) != static_cast<size_t>(bsize)) { rc = 1; break; }
+      }
+    if (rc) break;
+    if (decode_stripes_impl(ext_of(plan), ptr.data(), 1, bsize, erasures)) { rc = 1; break; }
+    for (int i = 0; i < k; ++i) {
+      if (!missing[i]) continue;
+      const long long bpos = apos + i * plan->strip_size;
+      fseek(fd, bpos, SEEK_SET);
+      // the last data strip is truncated to the file size (erasure_tools.c:576-582)
+      const long long len = (i == k - 1 && bpos + bsize > fsize) ? fsize - bpos : bsize;
+      if (len > 0 && fwrite(ptr[i], 1, len, fd) != static_cast<size_t>(len)) rc = 1;
+    }
+  }
+  fclose(fd);
+  fclose(fp);
+  return rc;
+}
+
+// ---- extensions
+int et_encode_stripes(lio_erasure_plan_t *plan, char **ptrs, int nstripes, int block_size) {
+  PlanExt *e = ext_of(plan);
+  if (!e) return fail("not an lstore_ec plan");
+  return encode_stripes_impl(e, ptrs, nstripes, block_size);
+}
+
+int et_decode_stripes(lio_erasure_plan_t *plan, char **ptrs, int nstripes, int block_size, int *erasures) {
+  PlanExt *e = ext_of(plan);
+  if (!e) return fail("not an lstore_ec plan");
+  return decode_stripes_impl(e, ptrs, nstripes, block_size, erasures);
+}
+
+int lsec_encode_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int nstripes, long long block_size,
+                    void *stream) {
+  PlanExt *e = ext_of(plan);
+  if (!e) return fail("not an lstore_ec plan");
+  if (!shards) return fail("shards is NULL");
+  return encode_dev(e, shards, nstripes, block_size, static_cast<hipStream_t>(stream));
+}
+
+int lsec_decode_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int nstripes, long long block_size,
+                    const int *erasures, void *stream) {
+  PlanExt *e = ext_of(plan);
+  if (!e) return fail("not an lstore_ec plan");
+  if (!shards) return fail("shards is NULL");
+  return decode_dev(e, shards, nstripes, block_size, erasures, static_cast<hipStream_t>(stream));
+}
+
+int lsec_prepare_decode(lio_erasure_plan_t *plan, const int *erasures) {
+  PlanExt *e = ext_of(plan);
+  if (!e) return fail("not an lstore_ec plan");
+  std::vector<int> ids;
+  const int pr = parse_erasures(plan, erasures, ids);
+  if (pr != 0) return pr < 0 ? -1 : 0;
+  DecodeEntry *ent = nullptr;
+  CoefCell *cells = nullptr;
+  return decode_entry(e, ids, &ent, &cells);
+}
+
+int lsec_abi_version(void) { return LSEC_ABI_VERSION; }
+
+int lsec_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+const char *lsec_last_error(void) { return tl_err.c_str(); }
+
+int lsec_plan_kernel(lio_erasure_plan_t *plan) { return plan ? kernel_kind(plan->method, plan->w) : 0; }
+
+void lsec_set_kernel_variant(int bytewise_variant, int bitsliced_variant) {
+  lsec::set_kernel_variant(bytewise_variant, bitsliced_variant);
+}
+
+}  // extern "C"

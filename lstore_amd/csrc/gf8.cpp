@@ -1,0 +1,362 @@
+// gf8.cpp -- host-side GF(2^8) algebra for the plan service.  See gf8.h.
+#include "gf8.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace lsec {
+namespace gf8 {
+
+namespace {
+
+struct Tables {
+  uint8_t exp[512];
+  int16_t log[256];
+  uint8_t prod[256][256];
+  Tables() {
+    unsigned x = 1;
+    for (int i = 0; i < 255; ++i) {
+      exp[i] = exp[i + 255] = static_cast<uint8_t>(x);
+      log[x] = static_cast<int16_t>(i);
+      x <<= 1;
+      if (x & 0x100) x ^= 0x11D;
+    }
+    exp[510] = exp[511] = exp[0];
+    log[0] = -1;
+    for (int a = 0; a < 256; ++a)
+      for (int b = 0; b < 256; ++b)
+        prod[a][b] = (a && b) ? exp[log[a] + log[b]] : 0;
+  }
+};
+
+const Tables &T() {
+  static const Tables t;  // thread-safe static init (C++11)
+  return t;
+}
+
+}  // namespace
+
+uint8_t mul(uint8_t a, uint8_t b) { return T().prod[a][b]; }
+uint8_t div(uint8_t a, uint8_t b) { return a ? T().exp[T().log[a] + 255 - T().log[b]] : 0; }
+uint8_t inv(uint8_t a) { return T().exp[255 - T().log[a]]; }
+
+// ---------------------------------------------------------------- Reed-Solomon
+// The systematic Vandermonde "distribution matrix" of Jerasure (reed_sol.c:242-367):
+// start from the extended Vandermonde matrix V[(k+m) x k] (row 0 = e0, last row = e_{k-1},
+// row i = powers of i), column-reduce the top k x k block to the identity, scale every
+// column so that row k is all ones, then scale each later row so its column 0 is one.
+bool reed_sol_vandermonde(int k, int m, Mat &out) {
+  const int rows = k + m;
+  if (k < 1 || m < 1 || rows > 256) return false;
+  std::vector<uint8_t> v(static_cast<size_t>(rows) * k, 0);
+  auto at = [&](int r, int c) -> uint8_t & { return v[static_cast<size_t>(r) * k + c]; };
+  at(0, 0) = 1;
+  at(rows - 1, k - 1) = 1;
+  for (int r = 1; r < rows - 1; ++r) {
+    uint8_t p = 1;
+    for (int c = 0; c < k; ++c) { at(r, c) = p; p = mul(p, static_cast<uint8_t>(r)); }
+  }
+  for (int piv = 1; piv < k; ++piv) {
+    int r = piv;
+    while (r < rows && at(r, piv) == 0) ++r;
+    if (r == rows) return false;
+    if (r != piv)
+      for (int c = 0; c < k; ++c) std::swap(at(r, c), at(piv, c));
+    if (at(piv, piv) != 1) {
+      const uint8_t s = inv(at(piv, piv));
+      for (int rr = 0; rr < rows; ++rr) at(rr, piv) = mul(s, at(rr, piv));
+    }
+    for (int c = 0; c < k; ++c) {
+      const uint8_t e = at(piv, c);
+      if (c == piv || e == 0) continue;
+      for (int rr = 0; rr < rows; ++rr) at(rr, c) ^= mul(e, at(rr, piv));
+    }
+  }
+  for (int c = 0; c < k; ++c) {
+    const uint8_t e = at(k, c);
+    if (e == 1) continue;
+    const uint8_t s = inv(e);
+    for (int rr = k; rr < rows; ++rr) at(rr, c) = mul(s, at(rr, c));
+  }
+  for (int rr = k + 1; rr < rows; ++rr) {
+    const uint8_t e = at(rr, 0);
+    if (e == 1) continue;
+    const uint8_t s = inv(e);
+    for (int c = 0; c < k; ++c) at(rr, c) = mul(at(rr, c), s);
+  }
+  out.assign(v.begin() + static_cast<size_t>(k) * k, v.end());
+  return true;
+}
+
+bool reed_sol_r6(int k, Mat &out) {
+  if (k < 1 || k > 255) return false;
+  out.assign(2 * static_cast<size_t>(k), 1);
+  uint8_t p = 1;
+  for (int j = 0; j < k; ++j) { out[k + j] = p; p = mul(p, 2); }
+  return true;
+}
+
+// ---------------------------------------------------------------- Cauchy
+int bit_block_ones(uint8_t e) {
+  int n = 0;
+  for (int x = 0; x < 8; ++x) { n += __builtin_popcount(e); e = mul(e, 2); }
+  return n;
+}
+
+bool cauchy_original(int k, int m, Mat &out) {
+  if (k < 1 || m < 1 || k + m > 256) return false;
+  out.resize(static_cast<size_t>(k) * m);
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < k; ++j) out[i * k + j] = inv(static_cast<uint8_t>(i ^ (m + j)));
+  return true;
+}
+
+void cauchy_improve(int k, int m, Mat &a) {
+  for (int j = 0; j < k; ++j) {           // make row 0 all ones (column scaling)
+    if (a[j] == 1) continue;
+    const uint8_t s = inv(a[j]);
+    for (int i = 0; i < m; ++i) a[i * k + j] = mul(a[i * k + j], s);
+  }
+  for (int i = 1; i < m; ++i) {           // then pick, per row, the scaling with fewest ones
+    uint8_t *row = &a[static_cast<size_t>(i) * k];
+    int best = 0, best_col = -1;
+    for (int j = 0; j < k; ++j) best += bit_block_ones(row[j]);
+    for (int j = 0; j < k; ++j) {
+      if (row[j] == 1) continue;
+      const uint8_t s = inv(row[j]);
+      int ones = 0;
+      for (int x = 0; x < k; ++x) ones += bit_block_ones(mul(row[x], s));
+      if (ones < best) { best = ones; best_col = j; }
+    }
+    if (best_col >= 0) {
+      const uint8_t s = inv(row[best_col]);
+      for (int j = 0; j < k; ++j) row[j] = mul(row[j], s);
+    }
+  }
+}
+
+// Second rows of the optimal m = 2 Cauchy matrices for w = 8: a table of constants from
+// vendor/jerasure/src/cauchy.c:262-274 (cbest_8), indexed by data column.
+static const uint8_t kCauchyBestW8[255] = {
+    1,   2,   142, 4,   71,  8,   70,  173, 3,   35,  143, 16,  17,  67,  134, 140, 172, 6,   34,
+    69,  201, 216, 5,   33,  86,  12,  65,  138, 158, 159, 175, 10,  32,  43,  66,  108, 130, 193,
+    234, 9,   24,  25,  50,  68,  79,  100, 132, 174, 200, 217, 20,  21,  42,  48,  87,  169, 41,
+    54,  64,  84,  96,  117, 154, 155, 165, 226, 77,  82,  135, 136, 141, 168, 192, 218, 238, 7,
+    18,  19,  39,  40,  78,  113, 116, 128, 164, 180, 195, 205, 220, 232, 14,  26,  27,  58,  109,
+    156, 157, 203, 235, 13,  28,  29,  38,  51,  56,  75,  85,  90,  101, 110, 112, 139, 171, 11,
+    37,  49,  52,  76,  83,  102, 119, 131, 150, 151, 167, 182, 184, 188, 197, 219, 224, 45,  55,
+    80,  94,  97,  133, 170, 194, 204, 221, 227, 236, 36,  47,  73,  92,  98,  104, 118, 152, 153,
+    166, 202, 207, 239, 251, 22,  23,  44,  74,  91,  148, 149, 161, 181, 190, 233, 46,  59,  88,
+    137, 146, 147, 163, 196, 208, 212, 222, 250, 57,  81,  95,  106, 111, 129, 160, 176, 199, 243,
+    249, 15,  53,  72,  93,  103, 115, 125, 162, 183, 185, 189, 206, 225, 255, 186, 210, 230, 237,
+    242, 248, 30,  31,  62,  89,  99,  105, 114, 121, 124, 178, 209, 213, 223, 228, 241, 254, 60,
+    191, 198, 247, 120, 240, 107, 127, 144, 145, 177, 211, 214, 246, 245, 123, 126, 187, 231, 253,
+    63,  179, 229, 244, 61,  122, 215, 252};
+
+bool cauchy_good(int k, int m, Mat &out) {
+  if (m == 2 && k >= 1 && k <= 255) {
+    out.assign(2 * static_cast<size_t>(k), 1);
+    std::memcpy(&out[k], kCauchyBestW8, k);
+    return true;
+  }
+  if (!cauchy_original(k, m, out)) return false;
+  cauchy_improve(k, m, out);
+  return true;
+}
+
+std::vector<int> to_bitmatrix(int k, int m, const Mat &a) {
+  const int cols = k * 8;
+  std::vector<int> bm(static_cast<size_t>(m) * 8 * cols, 0);
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < k; ++j) {
+      uint8_t e = a[i * k + j];
+      for (int x = 0; x < 8; ++x, e = mul(e, 2))
+        for (int l = 0; l < 8; ++l) bm[static_cast<size_t>(i * 8 + l) * cols + j * 8 + x] = (e >> l) & 1;
+    }
+  return bm;
+}
+
+// ---------------------------------------------------------------- schedule
+// Greedy "smart" scheduling of Jerasure (jerasure.c:1241-1360): emit output rows in
+// order of fewest remaining XORs; a row may start from a copy of an already emitted
+// row (from[]) when that is cheaper than starting from scratch.  Reproduced op for op
+// because plan->encode_schedule is part of the ABI the segment layer can see.
+std::vector<std::array<int, 5>> smart_schedule(int k, int m, int w, const std::vector<int> &bm) {
+  const int rows = m * w, cols = k * w;
+  std::vector<std::array<int, 5>> ops;
+  std::vector<int> diff(rows), from(rows, -1), next(rows), prev(rows);
+  int best_row = -1, best = cols + 1;
+  for (int r = 0; r < rows; ++r) {
+    int ones = 0;
+    for (int c = 0; c < cols; ++c) ones += bm[static_cast<size_t>(r) * cols + c];
+    diff[r] = ones;
+    next[r] = r + 1;
+    prev[r] = r - 1;
+    if (ones < best) { best = ones; best_row = r; }
+  }
+  next[rows - 1] = -1;
+  int head = 0;
+  while (head != -1) {
+    const int row = best_row;
+    if (prev[row] == -1) {                        // unlink row
+      head = next[row];
+      if (head != -1) prev[head] = -1;
+    } else {
+      next[prev[row]] = next[row];
+      if (next[row] != -1) prev[next[row]] = prev[row];
+    }
+    const int *cur = &bm[static_cast<size_t>(row) * cols];
+    if (from[row] == -1) {
+      int x = 0;
+      for (int c = 0; c < cols; ++c)
+        if (cur[c]) { ops.push_back({c / w, c % w, k + row / w, row % w, x}); x = 1; }
+    } else {
+      ops.push_back({k + from[row] / w, from[row] % w, k + row / w, row % w, 0});
+      const int *base = &bm[static_cast<size_t>(from[row]) * cols];
+      for (int c = 0; c < cols; ++c)
+        if (cur[c] ^ base[c]) ops.push_back({c / w, c % w, k + row / w, row % w, 1});
+    }
+    best = cols + 1;
+    for (int r = head; r != -1; r = next[r]) {
+      const int *other = &bm[static_cast<size_t>(r) * cols];
+      int d = 1;
+      for (int c = 0; c < cols; ++c) d += cur[c] ^ other[c];
+      if (d < diff[r]) { from[r] = row; diff[r] = d; }
+      if (diff[r] < best) { best = diff[r]; best_row = r; }
+    }
+  }
+  return ops;
+}
+
+// ---------------------------------------------------------------- inversion / decode
+bool invert(int n, Mat a, Mat &out) {
+  out.assign(static_cast<size_t>(n) * n, 0);
+  for (int i = 0; i < n; ++i) out[i * n + i] = 1;
+  for (int c = 0; c < n; ++c) {
+    int p = c;
+    while (p < n && a[p * n + c] == 0) ++p;
+    if (p == n) return false;
+    if (p != c)
+      for (int x = 0; x < n; ++x) { std::swap(a[p * n + x], a[c * n + x]); std::swap(out[p * n + x], out[c * n + x]); }
+    const uint8_t s = inv(a[c * n + c]);
+    for (int x = 0; x < n; ++x) { a[c * n + x] = mul(a[c * n + x], s); out[c * n + x] = mul(out[c * n + x], s); }
+    for (int r = 0; r < n; ++r) {
+      const uint8_t f = a[r * n + c];
+      if (r == c || f == 0) continue;
+      for (int x = 0; x < n; ++x) { a[r * n + x] ^= mul(f, a[c * n + x]); out[r * n + x] ^= mul(f, out[c * n + x]); }
+    }
+  }
+  return true;
+}
+
+bool make_decode(int k, int m, const Mat &coding, const std::vector<int> &erased_ids, DecodePlan &dp) {
+  std::vector<char> lost(k + m, 0);
+  for (int e : erased_ids) {
+    if (e < 0 || e >= k + m) return false;
+    lost[e] = 1;
+  }
+  dp.erased.clear();
+  dp.survivors.clear();
+  for (int i = 0; i < k + m; ++i) {
+    if (lost[i]) dp.erased.push_back(i);
+    else if (static_cast<int>(dp.survivors.size()) < k) dp.survivors.push_back(i);
+  }
+  if (static_cast<int>(dp.survivors.size()) < k) return false;
+  // S (k x k): row j expresses survivor j in terms of the data devices
+  Mat s(static_cast<size_t>(k) * k, 0), sinv;
+  for (int j = 0; j < k; ++j) {
+    const int id = dp.survivors[j];
+    if (id < k) s[j * k + id] = 1;
+    else std::memcpy(&s[static_cast<size_t>(j) * k], &coding[static_cast<size_t>(id - k) * k], k);
+  }
+  if (!invert(k, s, sinv)) return false;
+  // data_i = row i of S^-1 . survivors;  coding_i = C_i . data = (C_i . S^-1) . survivors
+  dp.rows.assign(dp.erased.size() * k, 0);
+  for (size_t r = 0; r < dp.erased.size(); ++r) {
+    const int id = dp.erased[r];
+    uint8_t *dst = &dp.rows[r * k];
+    if (id < k) {
+      std::memcpy(dst, &sinv[static_cast<size_t>(id) * k], k);
+    } else {
+      const uint8_t *crow = &coding[static_cast<size_t>(id - k) * k];
+      for (int j = 0; j < k; ++j) {
+        uint8_t acc = 0;
+        for (int t = 0; t < k; ++t) acc ^= mul(crow[t], sinv[t * k + j]);
+        dst[j] = acc;
+      }
+    }
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------- liberation family
+// Layout helper: a (2w) x (kw) bitmatrix whose first w rows are [I I ... I].
+static std::vector<int> identity_top(int k, int w) {
+  std::vector<int> bm(2 * static_cast<size_t>(k) * w * w, 0);
+  for (int i = 0; i < w; ++i)
+    for (int j = 0; j < k; ++j) bm[static_cast<size_t>(i) * k * w + j * w + i] = 1;
+  return bm;
+}
+
+std::vector<int> liberation_bitmatrix(int k, int w) {
+  if (k > w) return {};
+  std::vector<int> bm = identity_top(k, w);
+  const size_t q = static_cast<size_t>(k) * w * w;  // start of the Q block row
+  const int kw = k * w;
+  for (int j = 0; j < k; ++j) {
+    for (int i = 0; i < w; ++i) bm[q + static_cast<size_t>(i) * kw + j * w + (j + i) % w] = 1;
+    if (j > 0) {
+      const int i = (j * ((w - 1) / 2)) % w;
+      bm[q + static_cast<size_t>(i) * kw + j * w + (i + j - 1) % w] = 1;
+    }
+  }
+  return bm;
+}
+
+// liber8tion Q block (liberation.c:167-265, constants): for data column j, row r of the
+// 8x8 block has a one at column kLib8Perm[j][r]; plus one extra bit kLib8Extra[j] =
+// {row, col} for j >= 1.
+static const int8_t kLib8Perm[8][8] = {
+    {0, 1, 2, 3, 4, 5, 6, 7}, {7, 3, 0, 2, 6, 1, 5, 4}, {6, 2, 4, 0, 7, 3, 1, 5},
+    {2, 5, 7, 6, 0, 3, 4, 1}, {5, 6, 1, 7, 2, 4, 3, 0}, {1, 2, 3, 4, 5, 6, 7, 0},
+    {3, 0, 6, 5, 1, 7, 4, 2}, {4, 7, 1, 5, 3, 2, 0, 6}};
+static const int8_t kLib8Extra[8][2] = {{-1, -1}, {4, 7}, {1, 3}, {5, 4}, {2, 0}, {7, 2}, {6, 5}, {3, 1}};
+
+std::vector<int> liber8tion_bitmatrix(int k) {
+  const int w = 8;
+  if (k > w) return {};
+  std::vector<int> bm = identity_top(k, w);
+  const size_t q = static_cast<size_t>(k) * w * w;
+  const int kw = k * w;
+  for (int j = 0; j < k; ++j) {
+    for (int r = 0; r < 8; ++r) bm[q + static_cast<size_t>(r) * kw + j * w + kLib8Perm[j][r]] = 1;
+    if (kLib8Extra[j][0] >= 0) bm[q + static_cast<size_t>(kLib8Extra[j][0]) * kw + j * w + kLib8Extra[j][1]] = 1;
+  }
+  return bm;
+}
+
+std::vector<int> blaum_roth_bitmatrix(int k, int w) {
+  if (k > w) return {};
+  std::vector<int> bm = identity_top(k, w);
+  const size_t q = static_cast<size_t>(k) * w * w;
+  const int kw = k * w, p = w + 1;
+  for (int j = 0; j < k; ++j) {
+    for (int l = 1; l <= w; ++l) {
+      int *row = &bm[q + static_cast<size_t>(l - 1) * kw + j * w];
+      if (j == 0) { row[l - 1] = 1; continue; }
+      if (l != p - j) {
+        int c = l + j;
+        if (c >= p) c -= p;
+        row[c - 1] = 1;
+      } else {
+        row[j - 1] = 1;
+        const int c = (j % 2 == 0) ? j / 2 : (p / 2) + 1 + (j / 2);
+        row[c - 1] = 1;
+      }
+    }
+  }
+  return bm;
+}
+
+}  // namespace gf8
+}  // namespace lsec

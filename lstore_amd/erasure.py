@@ -1,0 +1,342 @@
+"""Python mirror of LStore's erasure plan service (src/lio/erasure_tools.h) over liblstore_ec.so.
+
+``Plan`` owns one ``lio_erasure_plan_t*`` created by the library and exposes
+
+* the reference API one-to-one: ``Plan.generate`` (et_generate_plan), ``Plan.new``
+  (et_new_plan), ``form_encoding_matrix`` / ``form_decoding_matrix`` / ``encode_block`` /
+  ``decode_block`` called *through the struct's function pointers*, exactly as
+  src/lio/segment/jerasure.c:1847 / :245 / :2242-2243 call them, plus the struct fields;
+* the batched extensions (``encode_stripes`` / ``decode_stripes``) and the device-resident
+  calls (``encode_dev`` / ``decode_dev``) that take torch CUDA tensors or raw shard refs.
+
+Errors mirror the reference: calls that return a status in C raise ``ErasureError`` with
+the library's message when the status is non-zero.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import Iterable, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+_LIB_PATH = os.path.join(HERE, "liblstore_ec.so")
+
+# method ids -- src/lio/erasure_tools.h:37-45
+REED_SOL_VAN, REED_SOL_R6_OP, CAUCHY_ORIG, CAUCHY_GOOD, BLAUM_ROTH, LIBERATION, LIBER8TION, RAID4 = range(8)
+JE_METHOD_NAMES = ("reed_sol_van", "reed_sol_r6_op", "cauchy_orig", "cauchy_good", "blaum_roth",
+                   "liberation", "liber8tion", "raid4")
+
+
+class ErasureError(RuntimeError):
+    pass
+
+
+# ----------------------------------------------------------------------------- ABI mirror
+class PlanStruct(C.Structure):
+    """src/lio/erasure_tools.h:50-65"""
+
+
+_FORM = C.CFUNCTYPE(C.c_int, C.POINTER(PlanStruct))
+_ENC = C.CFUNCTYPE(None, C.POINTER(PlanStruct), C.POINTER(C.c_void_p), C.c_int)
+_DEC = C.CFUNCTYPE(C.c_int, C.POINTER(PlanStruct), C.POINTER(C.c_void_p), C.c_int, C.POINTER(C.c_int))
+
+PlanStruct._fields_ = [
+    ("strip_size", C.c_longlong),
+    ("method", C.c_int),
+    ("data_strips", C.c_int),
+    ("parity_strips", C.c_int),
+    ("w", C.c_int),
+    ("packet_size", C.c_int),
+    ("base_unit", C.c_int),
+    ("encode_matrix", C.POINTER(C.c_int)),
+    ("encode_bitmatrix", C.POINTER(C.c_int)),
+    ("encode_schedule", C.POINTER(C.POINTER(C.c_int))),
+    ("form_encoding_matrix", _FORM),
+    ("form_decoding_matrix", _FORM),
+    ("encode_block", _ENC),
+    ("decode_block", _DEC),
+]
+
+
+class ShardRef(C.Structure):
+    """lsec_shard_t: shard i of stripe s lives at base + s*stride (device memory)."""
+    _fields_ = [("base", C.c_void_p), ("stride", C.c_longlong)]
+
+
+# every function include/lstore_ec.h declares (tests check the .so exports all of them)
+EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan", "et_destroy_plan",
+           "et_encode", "et_decode", "et_encode_stripes", "et_decode_stripes", "lsec_encode_dev",
+           "lsec_decode_dev", "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count",
+           "lsec_last_error", "lsec_plan_kernel", "lsec_set_kernel_variant")
+
+_lib = None
+
+
+def library_path() -> str:
+    return _LIB_PATH
+
+
+def build_library(force: bool = False) -> str:
+    """Compile liblstore_ec.so for gfx950 in-tree (hipcc)."""
+    if force or not os.path.exists(_LIB_PATH):
+        jobs = str(min(8, os.cpu_count() or 1))
+        subprocess.run(["make", "-s", "-j", jobs, "-C", os.path.join(HERE, "csrc")], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    """Load liblstore_ec.so.  There is no fallback: a missing library is an error."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise ErasureError(f"{_LIB_PATH} is not built; run lstore_amd.build_library() "
+                           "(or `make -C lstore_amd/csrc`)")
+    L = C.CDLL(_LIB_PATH)
+    P = C.POINTER(PlanStruct)
+    L.et_generate_plan.restype = P
+    L.et_generate_plan.argtypes = [C.c_longlong, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+    L.et_new_plan.restype = P
+    L.et_new_plan.argtypes = [C.c_int, C.c_longlong, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+    L.et_destroy_plan.argtypes = [P]
+    L.et_destroy_plan.restype = None
+    L.et_method_type.argtypes = [C.c_char_p]
+    L.nearest_prime.argtypes = [C.c_int, C.c_int]
+    L.et_encode.argtypes = [P, C.c_char_p, C.c_longlong, C.c_char_p, C.c_longlong, C.c_int]
+    L.et_decode.argtypes = [P, C.c_longlong, C.c_char_p, C.c_longlong, C.c_char_p, C.c_longlong, C.c_int,
+                            C.POINTER(C.c_int)]
+    L.et_encode_stripes.argtypes = [P, C.POINTER(C.c_void_p), C.c_int, C.c_int]
+    L.et_decode_stripes.argtypes = [P, C.POINTER(C.c_void_p), C.c_int, C.c_int, C.POINTER(C.c_int)]
+    L.lsec_encode_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.c_void_p]
+    L.lsec_decode_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.POINTER(C.c_int), C.c_void_p]
+    L.lsec_prepare_decode.argtypes = [P, C.POINTER(C.c_int)]
+    L.lsec_last_error.restype = C.c_char_p
+    L.lsec_plan_kernel.argtypes = [P]
+    L.lsec_set_kernel_variant.argtypes = [C.c_int, C.c_int]
+    L.lsec_set_kernel_variant.restype = None
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    return (lib().lsec_last_error() or b"").decode()
+
+
+def _check(rc: int, what: str) -> int:
+    if rc != 0:
+        raise ErasureError(f"{what} failed (rc={rc}): {last_error()}")
+    return rc
+
+
+def _erasure_array(erasures: Iterable[int]):
+    vals = list(erasures) + [-1]
+    return (C.c_int * len(vals))(*vals)
+
+
+def nearest_prime(w: int, which: int) -> int:
+    return lib().nearest_prime(w, which)
+
+
+def method_type(name: str) -> int:
+    return lib().et_method_type(name.encode())
+
+
+# ----------------------------------------------------------------------------- plan
+class Plan:
+    """One lio_erasure_plan_t owned by liblstore_ec.so."""
+
+    def __init__(self, ptr):
+        if not ptr:
+            raise ErasureError(f"plan creation failed: {last_error()}")
+        self._p = ptr
+
+    # -- constructors (et_generate_plan / et_new_plan)
+    @classmethod
+    def generate(cls, file_size, method, k, m, w=-1, packet_low=-1, packet_high=-1) -> "Plan":
+        return cls(lib().et_generate_plan(file_size, method, k, m, w, packet_low, packet_high))
+
+    @classmethod
+    def new(cls, method, strip_size, k, m, w, packet_size, base_unit=8) -> "Plan":
+        return cls(lib().et_new_plan(method, strip_size, k, m, w, packet_size, base_unit))
+
+    @classmethod
+    def for_chunk(cls, method, k, m, chunk) -> "Plan":
+        """The plan segment/jerasure.c:2236-2243 builds: et_generate_plan(k*C, ...) + form_*."""
+        p = cls.generate(k * chunk, method, k, m)
+        p.form_encoding_matrix()
+        p.form_decoding_matrix()
+        return p
+
+    def close(self):
+        if getattr(self, "_p", None):
+            lib().et_destroy_plan(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- struct fields
+    @property
+    def ptr(self):
+        return self._p
+
+    @property
+    def s(self) -> PlanStruct:
+        return self._p.contents
+
+    k = property(lambda self: self.s.data_strips)
+    m = property(lambda self: self.s.parity_strips)
+    w = property(lambda self: self.s.w)
+    method = property(lambda self: self.s.method)
+    packet_size = property(lambda self: self.s.packet_size)
+    strip_size = property(lambda self: self.s.strip_size)
+    base_unit = property(lambda self: self.s.base_unit)
+
+    @property
+    def kernel(self) -> int:
+        """1 = bytewise (matrix codes), 2 = bitsliced (Cauchy), 0 = no GPU kernel"""
+        return lib().lsec_plan_kernel(self._p)
+
+    def matrix(self):
+        if not self.s.encode_matrix:
+            return None
+        rows = 2 if self.method == REED_SOL_R6_OP else self.m
+        n = rows * self.k
+        return np.ctypeslib.as_array(self.s.encode_matrix, shape=(n,)).copy().reshape(rows, self.k)
+
+    def bitmatrix(self):
+        if not self.s.encode_bitmatrix:
+            return None
+        n = self.k * self.m * self.w * self.w
+        return np.ctypeslib.as_array(self.s.encode_bitmatrix, shape=(n,)).copy().reshape(self.m * self.w, -1)
+
+    def schedule(self):
+        if not self.s.encode_schedule:
+            return None
+        ops, i = [], 0
+        while True:
+            row = self.s.encode_schedule[i]
+            if row[0] == -1:
+                break
+            ops.append([row[x] for x in range(5)])
+            i += 1
+        return np.array(ops, dtype=np.int32).reshape(-1, 5)
+
+    # -- fn-pointer calls (what the segment driver does)
+    def form_encoding_matrix(self) -> int:
+        return self.s.form_encoding_matrix(self._p)
+
+    def form_decoding_matrix(self) -> int:
+        return self.s.form_decoding_matrix(self._p)
+
+    @staticmethod
+    def _ptr_array(addrs: Sequence[int]):
+        return (C.c_void_p * len(addrs))(*addrs)
+
+    def encode_block(self, shards: Sequence[np.ndarray] | Sequence[int], block_size: int | None = None):
+        """plan->encode_block(plan, ptr, C); shards = k+m host arrays (or raw addresses)."""
+        addrs = [s if isinstance(s, int) else s.ctypes.data for s in shards]
+        if block_size is None:
+            block_size = shards[0].nbytes
+        self.s.encode_block(self._p, self._ptr_array(addrs), block_size)
+
+    def decode_block(self, shards, erasures: Iterable[int], block_size: int | None = None) -> int:
+        """plan->decode_block(...) -> rc (0 / -1), like the reference (no exception)."""
+        addrs = [s if isinstance(s, int) else s.ctypes.data for s in shards]
+        if block_size is None:
+            block_size = shards[0].nbytes
+        return self.s.decode_block(self._p, self._ptr_array(addrs), block_size, _erasure_array(erasures))
+
+    # -- batched host calls
+    def _stripe_ptrs(self, stripes: np.ndarray):
+        n, km, size = stripes.shape
+        assert km == self.k + self.m and stripes.dtype == np.uint8 and stripes.flags.c_contiguous
+        base = stripes.ctypes.data
+        addrs = [base + (s * km + i) * size for s in range(n) for i in range(km)]
+        return self._ptr_array(addrs), n, size
+
+    def encode_stripes(self, stripes: np.ndarray) -> None:
+        """stripes: uint8 [N, k+m, C] host array; parity rows are overwritten."""
+        arr, n, size = self._stripe_ptrs(stripes)
+        _check(lib().et_encode_stripes(self._p, arr, n, size), "et_encode_stripes")
+
+    def decode_stripes(self, stripes: np.ndarray, erasures: Iterable[int]) -> None:
+        arr, n, size = self._stripe_ptrs(stripes)
+        _check(lib().et_decode_stripes(self._p, arr, n, size, _erasure_array(erasures)), "et_decode_stripes")
+
+    def encode_stripes_ptrs(self, ptr_array, nstripes: int, block_size: int) -> None:
+        _check(lib().et_encode_stripes(self._p, ptr_array, nstripes, block_size), "et_encode_stripes")
+
+    def decode_stripes_ptrs(self, ptr_array, nstripes: int, block_size: int, erasures) -> None:
+        _check(lib().et_decode_stripes(self._p, ptr_array, nstripes, block_size, _erasure_array(erasures)),
+               "et_decode_stripes")
+
+    # -- device-resident calls
+    @staticmethod
+    def shard_refs(refs: Sequence[tuple[int, int]]):
+        arr = (ShardRef * len(refs))()
+        for i, (base, stride) in enumerate(refs):
+            arr[i].base = base
+            arr[i].stride = stride
+        return arr
+
+    def tensor_refs(self, data, parity):
+        """Shard refs for torch uint8 tensors data [N,k,C] and parity [N,m,C] (contiguous rows)."""
+        size = data.shape[-1]
+        refs = [(data.data_ptr() + j * data.stride(1), data.stride(0)) for j in range(self.k)]
+        refs += [(parity.data_ptr() + i * parity.stride(1), parity.stride(0)) for i in range(parity.shape[1])]
+        return refs, data.shape[0], size
+
+    def encode_dev_refs(self, refs, nstripes: int, block_size: int, stream: int = 0) -> None:
+        _check(lib().lsec_encode_dev(self._p, self.shard_refs(refs), nstripes, block_size, stream),
+               "lsec_encode_dev")
+
+    def decode_dev_refs(self, refs, nstripes: int, block_size: int, erasures, stream: int = 0) -> None:
+        _check(lib().lsec_decode_dev(self._p, self.shard_refs(refs), nstripes, block_size,
+                                     _erasure_array(erasures), stream), "lsec_decode_dev")
+
+    def encode_dev(self, data, parity, stream=None) -> None:
+        """torch: data uint8 [N,k,C], parity uint8 [N,m,C] on the current device."""
+        refs, n, size = self.tensor_refs(data, parity)
+        self.encode_dev_refs(refs, n, size, _stream_handle(stream))
+
+    def decode_dev(self, data, parity, erasures, stream=None, out=None) -> None:
+        """Rebuild erased shards of data/parity in place, or into ``out`` [N, e, C] (erased order)."""
+        refs, n, size = self.tensor_refs(data, parity)
+        if out is not None:
+            for r, e in enumerate(sorted(set(erasures))):
+                refs[e] = (out.data_ptr() + r * out.stride(1), out.stride(0))
+        self.decode_dev_refs(refs, n, size, erasures, _stream_handle(stream))
+
+    def prepare_decode(self, erasures) -> None:
+        _check(lib().lsec_prepare_decode(self._p, _erasure_array(erasures)), "lsec_prepare_decode")
+
+
+def _stream_handle(stream) -> int:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def device_count() -> int:
+    return lib().lsec_device_count()
+
+
+def set_kernel_variant(bytewise: int = 0, bitsliced: int = 0) -> None:
+    lib().lsec_set_kernel_variant(bytewise, bitsliced)
