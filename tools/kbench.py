@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Kernel A/B bench (development tool): interleaved rounds of encode/decode per kernel variant.
+
+python tools/kbench.py [--stripes N] [--rounds R] [--configs rs63,cg104,cg63]
+Prints HBM GB/s (algorithmic bytes / launch time, HIP events on the launch stream).
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import lstore_amd as L  # noqa: E402
+from lstore_amd import erasure as E  # noqa: E402
+
+CONFIGS = {
+    "rs63": (L.REED_SOL_VAN, 6, 3, 1 << 20),
+    "rs104": (L.REED_SOL_VAN, 10, 4, 1 << 20),
+    "cg63": (L.CAUCHY_GOOD, 6, 3, 1 << 20),
+    "cg104": (L.CAUCHY_GOOD, 10, 4, 4 << 20),
+    "rs206": (L.REED_SOL_VAN, 20, 6, 256 << 10),
+    "cg206": (L.CAUCHY_GOOD, 20, 6, 256 << 10),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--data-gib", type=float, default=24.0)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--configs", default="rs63,cg104,cg63")
+    ap.add_argument("--variants", default="0,0;1,0;0,2;0,4")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    variants = [tuple(int(x) for x in v.split(",")) for v in a.variants.split(";")]
+    for name in a.configs.split(","):
+        meth, k, m, C = CONFIGS[name]
+        N = max(8, int(a.data_gib * 2**30 / (k * C)))
+        plan = L.Plan.for_chunk(meth, k, m, C)
+        data = torch.randint(0, 256, (N, k, C), dtype=torch.uint8, device=dev)
+        par = torch.empty((N, m, C), dtype=torch.uint8, device=dev)
+        out = torch.empty((N, 1, C), dtype=torch.uint8, device=dev)
+        plan.encode_dev(data, par)
+        ref_par = par.clone()
+        stream = torch.cuda.current_stream()
+        res = {v: ([], []) for v in variants}
+        for _ in range(a.rounds):
+            for v in variants:
+                E.set_kernel_variant(*v)
+                e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                plan.encode_dev(data, par)
+                e0.record(stream)
+                for _ in range(a.reps):
+                    plan.encode_dev(data, par)
+                e1.record(stream)
+                for _ in range(a.reps):
+                    plan.decode_dev(data, par, [0], out=out)
+                e2.record(stream)
+                torch.cuda.synchronize()
+                res[v][0].append(e0.elapsed_time(e1) / a.reps)
+                res[v][1].append(e1.elapsed_time(e2) / a.reps)
+                assert torch.equal(par, ref_par), f"variant {v} changed parity"
+                assert torch.equal(out[:, 0], data[:, 0]), f"variant {v} decode mismatch"
+        for v in variants:
+            te = sorted(res[v][0])[len(res[v][0]) // 2]
+            td = sorted(res[v][1])[len(res[v][1]) // 2]
+            eb = (k + m) * C * N
+            db = (k + 1) * C * N
+            print(f"{name:6s} N={N:5d} variant={v}  encode {te:8.3f} ms {eb / te / 1e6:7.1f} GB/s "
+                  f"({eb / te / 8e9:5.1%})   decode {td:8.3f} ms {db / td / 1e6:7.1f} GB/s ({db / td / 8e9:5.1%})",
+                  flush=True)
+        E.set_kernel_variant(0, 0)
+        del data, par, out, ref_par
+        plan.close()
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
