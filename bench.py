@@ -83,6 +83,24 @@ def cpu_baseline(method_id, k, m, C, P, lost, budget_s):
             "encode_gibps": round(gib / t_enc, 3), "decode_gibps": round(gib / t_dec, 3), "decode_rc": rc}
 
 
+def pmc_traffic(k, m, C, N, kernel_kind):
+    """HBM bytes per encode launch from the committed rocprofv3 PMC measurement
+    (tools/pmc_traffic.py -> profiles/*_pmc_traffic.json), scaled to N stripes; None if no
+    measurement exists for this geometry."""
+    import glob
+
+    prefix = "void lsec::k_gf8_bytewise<%d," % m if kernel_kind == 1 else "void lsec::k_gf8_bitsliced<%d," % m
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
+        with open(f) as fh:
+            d = json.load(fh)
+        if (d.get("k"), d.get("m"), d.get("chunk")) != (k, m, C):
+            continue
+        for name, v in d["kernels"].items():
+            if name.startswith(prefix):
+                return int(v["traffic_per_stripe"] * N), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def host_path_rate(L, plan, k, m, C, lost, nstripes):
     """et_encode_stripes / et_decode_stripes from pageable host memory (PCIe-inclusive)."""
     tile = np.random.default_rng(2).integers(0, 256, size=(min(nstripes, 8), k + m, C), dtype=np.uint8)
@@ -114,9 +132,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        # one process per GPU; the only collectives are the timing barrier and the max-over-ranks
+        # reduction (RCCL by default; LSEC_DIST_BACKEND=gloo lets ranks share one GPU for rehearsal)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        backend = os.environ.get("LSEC_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -173,9 +197,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        from lstore_amd.partition import max_over_ranks
+        elapsed = max_over_ranks(elapsed, dev if dist.get_backend() == "nccl" else None)
 
     # ---- per-kernel timing with HIP events on the launch stream (roofline)
     reps = max(3, min(10, a.steps))
@@ -212,6 +235,7 @@ def main():
     enc_hbm = (k + m) * C * N
     dec_hbm = (k + 1) * C * N
     achieved = enc_hbm / t_enc
+    traffic, traffic_src = pmc_traffic(k, m, C, N, plan.kernel)
 
     out = None
     if rank == 0:
@@ -241,7 +265,8 @@ def main():
             "encode_gibps": round(data_bytes / t_enc / 2**30, 2),
             "decode_gibps": round(data_bytes / t_dec / 2**30, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "gf8_bytewise (encode)" if plan.kernel == 1 else "gf8_bitsliced (encode)",
                          "algorithmic_bytes_per_launch": enc_hbm, "avg_launch_ms": round(t_enc * 1e3, 4),
                          "decode_achieved_GBps": round(dec_hbm / t_dec / 1e9, 1),
