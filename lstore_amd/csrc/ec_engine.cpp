@@ -16,6 +16,8 @@
 #include <strings.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -24,6 +26,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lstore_ec.h"
@@ -392,27 +395,132 @@ int decode_dev(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C, co
   return enqueue_apply(kernel_kind(p->method, p->w), cells, k, R, in, out, nstripes, C, p->packet_size, st);
 }
 
+// ---------------------------------------------------------------- host copy pool
+// Host-memory callers hand over pageable buffers (cache pages, parity on the stack,
+// segment/jerasure.c:1315), so bytes must be packed into pinned staging before DMA.  One
+// CPU thread copies ~10 GB/s, well below PCIe Gen5, so packing/unpacking is spread over a
+// small process-wide worker pool (LSEC_COPY_THREADS, default min(8, cores)); the calling
+// thread works too.
+struct CopyJob {
+  char *dst;
+  const char *src;
+  size_t bytes;
+};
+
+class CopyPool {
+ public:
+  static CopyPool &get() {
+    static CopyPool *pool = new CopyPool();  // intentionally leaked: workers live until exit
+    return *pool;
+  }
+
+  void run(std::vector<CopyJob> &jobs) {
+    // split into pieces so every worker gets a share of large chunks
+    constexpr size_t kPiece = 512 << 10;
+    std::vector<CopyJob> pieces;
+    pieces.reserve(jobs.size());
+    for (const CopyJob &j : jobs)
+      for (size_t o = 0; o < j.bytes; o += kPiece)
+        pieces.push_back({j.dst + o, j.src + o, std::min(kPiece, j.bytes - o)});
+    if (pieces.empty()) return;
+    if (workers_.empty() || pieces.size() == 1) {
+      for (const CopyJob &j : pieces) std::memcpy(j.dst, j.src, j.bytes);
+      return;
+    }
+    Batch b;
+    b.jobs = pieces.data();
+    b.n = pieces.size();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      queue_.push_back(&b);
+    }
+    cv_.notify_all();
+    work(b, false);
+    std::unique_lock<std::mutex> lk(mu_);
+    auto it = std::find(queue_.begin(), queue_.end(), &b);
+    if (it != queue_.end()) queue_.erase(it);  // no new worker can pick it up now
+    done_cv_.wait(lk, [&] { return b.finished == b.n && b.users == 0; });
+  }
+
+ private:
+  struct Batch {
+    const CopyJob *jobs = nullptr;
+    size_t n = 0;
+    std::atomic<size_t> next{0};
+    size_t finished = 0;  // guarded by mu_
+    int users = 0;        // workers inside work() for this batch, guarded by mu_
+  };
+
+  CopyPool() {
+    const char *s = getenv("LSEC_COPY_THREADS");
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int n = s ? atoi(s) : static_cast<int>(std::min(8u, hw));
+    for (int i = 1; i < n; ++i) workers_.emplace_back([this] { loop(); });
+    for (auto &t : workers_) t.detach();
+  }
+
+  // copies pieces until none are left; the caller of work() must hold a `users` reference
+  void work(Batch &b, bool worker) {
+    size_t mine = 0;
+    for (size_t i; (i = b.next.fetch_add(1)) < b.n; ++mine) std::memcpy(b.jobs[i].dst, b.jobs[i].src, b.jobs[i].bytes);
+    std::lock_guard<std::mutex> lk(mu_);
+    b.finished += mine;
+    if (worker) --b.users;
+    if (b.finished == b.n && b.users == 0) done_cv_.notify_all();
+  }
+
+  void loop() {
+    for (;;) {
+      Batch *b = nullptr;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] {
+          for (Batch *q : queue_)
+            if (q->next.load() < q->n) return true;
+          return false;
+        });
+        for (Batch *q : queue_)
+          if (q->next.load() < q->n) { b = q; ++b->users; break; }
+      }
+      if (b) work(*b, true);
+    }
+  }
+
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<Batch *> queue_;
+};
+
 // ---------------------------------------------------------------- host staging pool
+// Each staging object owns a copy-in stream, a compute/copy-out stream and kSlots slots of
+// pinned + device memory, so that for consecutive batches  H2D(b+1) || kernel(b) -> D2H(b)
+// and the host packs b+2 / unpacks b-1 meanwhile (PCIe is full duplex).
+constexpr int kSlots = 3;
+
 struct Staging {
   int dev = -1;
-  hipStream_t stream = nullptr;
+  hipStream_t s_in = nullptr, s_out = nullptr;
   struct Slot {
     char *d = nullptr;   // device: [nb][nin][C] then [nb][nout][C]
     char *h = nullptr;   // pinned host, same layout
     size_t cap = 0;
-    hipEvent_t done = nullptr;
+    hipEvent_t in_done = nullptr, done = nullptr;
     bool pending = false;
     // what to unpack when `done` fires
     char **ptrs = nullptr;
     int s0 = 0, nb = 0;
-  } slot[2];
+    long long c0 = 0, clen = 0;  // column block of each shard this slot carries
+  } slot[kSlots];
   ~Staging() {
     for (auto &s : slot) {
       if (s.d) (void)hipFree(s.d);
       if (s.h) (void)hipHostFree(s.h);
       if (s.done) (void)hipEventDestroy(s.done);
+      if (s.in_done) (void)hipEventDestroy(s.in_done);
     }
-    if (stream) (void)hipStreamDestroy(stream);
+    if (s_in) (void)hipStreamDestroy(s_in);
+    if (s_out) (void)hipStreamDestroy(s_out);
   }
 };
 
@@ -431,12 +539,14 @@ Staging *acquire_staging(int dev) {
   }
   Staging *s = new Staging();
   s->dev = dev;
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&s->s_in, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&s->s_out, hipStreamNonBlocking) != hipSuccess) {
     delete s;
     return nullptr;
   }
   for (auto &sl : s->slot)
-    if (hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sl.in_done, hipEventDisableTiming) != hipSuccess) {
       delete s;
       return nullptr;
     }
@@ -464,7 +574,7 @@ int ensure_slot(Staging::Slot &sl, size_t bytes) {
 size_t staging_budget() {
   static size_t b = [] {
     const char *s = getenv("LSEC_STAGING_MB");
-    const long v = s ? atol(s) : 64;
+    const long v = s ? atol(s) : 128;
     return static_cast<size_t>(std::max(1L, v)) << 20;
   }();
   return b;
@@ -473,6 +583,11 @@ size_t staging_budget() {
 // Shared driver of the host-memory paths.  For each stripe, `in_ids` name the shards that
 // go to the GPU and `out_ids` the shards that come back (encode: data -> parity; decode:
 // survivors -> erased).  The kernel runs on the packed staging layout.
+//
+// Work is cut into batches of about half the staging budget: whole stripes when a stripe
+// fits, otherwise column blocks of every shard of one stripe (the codes act column-wise --
+// bytewise on any 8-byte boundary, bitsliced on super-packet boundaries -- so a block is a
+// valid independent sub-stripe).
 int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
              const std::vector<int> &out_ids, const CoefCell *cells, int kind) {
   lio_erasure_plan_t *p = &e->pub;
@@ -480,59 +595,84 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   const int nin = static_cast<int>(in_ids.size()), nout = static_cast<int>(out_ids.size());
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
+  const size_t budget = staging_budget();
+  const size_t per_col = static_cast<size_t>(nin + nout);  // staging bytes per column byte
+  long long cb = C;
+  if (per_col * C > budget / 2) {
+    const long long align = kind == KBITSLICED ? 8LL * p->packet_size : 8192;
+    cb = static_cast<long long>(budget / 2 / per_col) / align * align;
+    if (cb < align) cb = align;
+    if (cb >= C) cb = C;
+  }
+  const int nb_max = cb < C ? 1 : static_cast<int>(std::max<size_t>(1, std::min<size_t>(nstripes, budget / 2 / (per_col * C))));
+  const size_t slot_bytes = per_col * static_cast<size_t>(cb) * nb_max;
   Staging *stg = acquire_staging(dev);
-  if (!stg) return fail("cannot create staging stream");
-  const size_t per_stripe = static_cast<size_t>(nin + nout) * C;
-  const int nb_max = static_cast<int>(std::max<size_t>(1, std::min<size_t>(nstripes, staging_budget() / std::max<size_t>(per_stripe, 1))));
+  if (!stg) return fail("cannot create staging streams");
   int rc = 0;
+  std::vector<CopyJob> jobs;
 
   auto unpack = [&](Staging::Slot &sl) -> int {
     if (!sl.pending) return 0;
+    sl.pending = false;
     if (hipEventSynchronize(sl.done) != hipSuccess) return fail("staging event sync failed");
-    const char *outb = sl.h + static_cast<size_t>(sl.nb) * nin * C;
+    const size_t len = static_cast<size_t>(sl.clen);
+    const char *outb = sl.h + static_cast<size_t>(sl.nb) * nin * len;
+    jobs.clear();
     for (int s = 0; s < sl.nb; ++s)
       for (int r = 0; r < nout; ++r)
-        std::memcpy(sl.ptrs[static_cast<size_t>(sl.s0 + s) * km + out_ids[r]], outb + (static_cast<size_t>(s) * nout + r) * C, C);
-    sl.pending = false;
+        jobs.push_back({sl.ptrs[static_cast<size_t>(sl.s0 + s) * km + out_ids[r]] + sl.c0,
+                        outb + (static_cast<size_t>(s) * nout + r) * len, len});
+    CopyPool::get().run(jobs);
     return 0;
   };
 
   int which = 0;
-  for (int s0 = 0; s0 < nstripes && rc == 0; s0 += nb_max, which ^= 1) {
+  for (int s0 = 0; s0 < nstripes && rc == 0; s0 += nb_max) {
     const int nb = std::min(nb_max, nstripes - s0);
-    Staging::Slot &sl = stg->slot[which];
-    if ((rc = unpack(sl))) break;
-    if ((rc = ensure_slot(sl, per_stripe * nb_max))) break;
-    // pack inputs
-    for (int s = 0; s < nb; ++s)
+    for (long long c0 = 0; c0 < C && rc == 0; c0 += cb, which = (which + 1) % kSlots) {
+      const long long clen = std::min(cb, C - c0);
+      const size_t len = static_cast<size_t>(clen);
+      Staging::Slot &sl = stg->slot[which];
+      if ((rc = unpack(sl))) break;
+      if ((rc = ensure_slot(sl, slot_bytes))) break;
+      jobs.clear();
+      for (int s = 0; s < nb; ++s)
+        for (int j = 0; j < nin; ++j)
+          jobs.push_back({sl.h + (static_cast<size_t>(s) * nin + j) * len,
+                          ptrs[static_cast<size_t>(s0 + s) * km + in_ids[j]] + c0, len});
+      CopyPool::get().run(jobs);
+      const size_t in_bytes = static_cast<size_t>(nb) * nin * len;
+      const size_t out_off = in_bytes;
+      hipError_t err = hipMemcpyAsync(sl.d, sl.h, in_bytes, hipMemcpyHostToDevice, stg->s_in);
+      if (err == hipSuccess) err = hipEventRecord(sl.in_done, stg->s_in);
+      if (err == hipSuccess) err = hipStreamWaitEvent(stg->s_out, sl.in_done, 0);
+      if (err != hipSuccess) { rc = fail("H2D: %s", hipGetErrorString(err)); break; }
+      ShardRef in[lsec::kMaxK], out[64];
       for (int j = 0; j < nin; ++j)
-        std::memcpy(sl.h + (static_cast<size_t>(s) * nin + j) * C, ptrs[static_cast<size_t>(s0 + s) * km + in_ids[j]], C);
-    const size_t in_bytes = static_cast<size_t>(nb) * nin * C;
-    const size_t out_off = static_cast<size_t>(nb) * nin * C;
-    hipError_t err = hipMemcpyAsync(sl.d, sl.h, in_bytes, hipMemcpyHostToDevice, stg->stream);
-    if (err != hipSuccess) { rc = fail("H2D: %s", hipGetErrorString(err)); break; }
-    ShardRef in[lsec::kMaxK], out[64];
-    for (int j = 0; j < nin; ++j) in[j] = {reinterpret_cast<uint64_t>(sl.d) + static_cast<uint64_t>(j) * C, static_cast<int64_t>(nin) * C};
-    for (int r = 0; r < nout; ++r)
-      out[r] = {reinterpret_cast<uint64_t>(sl.d) + out_off + static_cast<uint64_t>(r) * C, static_cast<int64_t>(nout) * C};
-    if ((rc = enqueue_apply(kind, cells, nin, nout, in, out, nb, C, p->packet_size, stg->stream))) break;
-    err = hipMemcpyAsync(sl.h + out_off, sl.d + out_off, static_cast<size_t>(nb) * nout * C, hipMemcpyDeviceToHost, stg->stream);
-    if (err != hipSuccess) { rc = fail("D2H: %s", hipGetErrorString(err)); break; }
-    err = hipEventRecord(sl.done, stg->stream);
-    if (err != hipSuccess) { rc = fail("event record: %s", hipGetErrorString(err)); break; }
-    sl.pending = true;
-    sl.ptrs = ptrs;
-    sl.s0 = s0;
-    sl.nb = nb;
+        in[j] = {reinterpret_cast<uint64_t>(sl.d) + static_cast<uint64_t>(j) * len, static_cast<int64_t>(nin * len)};
+      for (int r = 0; r < nout; ++r)
+        out[r] = {reinterpret_cast<uint64_t>(sl.d) + out_off + static_cast<uint64_t>(r) * len, static_cast<int64_t>(nout * len)};
+      if ((rc = enqueue_apply(kind, cells, nin, nout, in, out, nb, clen, p->packet_size, stg->s_out))) break;
+      err = hipMemcpyAsync(sl.h + out_off, sl.d + out_off, static_cast<size_t>(nb) * nout * len, hipMemcpyDeviceToHost, stg->s_out);
+      if (err == hipSuccess) err = hipEventRecord(sl.done, stg->s_out);
+      if (err != hipSuccess) { rc = fail("D2H: %s", hipGetErrorString(err)); break; }
+      sl.pending = true;
+      sl.ptrs = ptrs;
+      sl.s0 = s0;
+      sl.nb = nb;
+      sl.c0 = c0;
+      sl.clen = clen;
+    }
   }
-  for (auto &sl : stg->slot) {
-    const int r2 = unpack(sl);
+  // drain in submission order
+  for (int i = 0; i < kSlots; ++i) {
+    const int r2 = unpack(stg->slot[(which + i) % kSlots]);
     if (!rc) rc = r2;
-    sl.pending = false;
   }
   if (rc) {
-    (void)hipStreamSynchronize(stg->stream);
-    delete stg;  // do not recycle a stream in an unknown state
+    (void)hipStreamSynchronize(stg->s_in);
+    (void)hipStreamSynchronize(stg->s_out);
+    delete stg;  // do not recycle streams in an unknown state
   } else {
     release_staging(stg);
   }

@@ -1,280 +1,12 @@
-// ec_kernels.hip -- gfx950 (CDNA4) erasure-coding kernels.  See ec_kernels.h for the contract.
-//
-// The path is HBM-bound byte/bit arithmetic (no MFMA):
-//   encode  reads K*C, writes R*C bytes per stripe
-//   decode  reads K survivors, writes R = #erased shards
-// Both kernels stream every input byte exactly once from HBM and write every output byte
-// exactly once; all GF(2^8) work happens in VGPRs.
-//
-// gf8_bytewise (Reed-Solomon / matrix codes).  Multiply-by-constant c of a byte v is split
-// over three bit fields of v:  c*v = c*(v & 7) ^ c*(v & 0x38) ^ c*(v & 0xC0).  Each field
-// has at most 8 values, so each partial product is ONE v_perm_b32 that selects bytes out of
-// an 8-byte table {c*0..c*7}, {c*0,c*8,..,c*56} or {c*0,c*64,c*128,c*192} -- four bytes of
-// the word at once.  The three field extractions are shared by all R outputs of an input
-// shard; per (output, input) pair a word costs 3 perms + 2 xors (v_xor3), versus a 64 KiB
-// table walk per byte on the CPU (galois.c:471-525).
-//
-// gf8_bitsliced (Cauchy / bitmatrix codes).  In Jerasure's packet layout the 8 bits of a
-// field element live in 8 different packets, so a 32-bit lane word of each packet carries
-// bit x of 32 independent elements.  Multiplying all of them by 2 is then a renaming of
-// the 8 packet words plus 3 XORs (x^8 = x^4+x^3+x^2+1), and c*e = sum_{t: c_t=1} 2^t e.
-// Per input shard: 7 doublings (21 xors per 8 words), then 8 xors per set coefficient bit,
-// under wave-uniform branches.  Identical result to running the smart XOR schedule over
-// the bitmatrix (jerasure.c:1168-1191), but every packet is read once and all
-// intermediates stay in registers instead of streaming P-byte XORs through memory.
-#include "ec_kernels.h"
+// ec_kernels.hip -- host-side launch policy for the gfx950 erasure kernels
+// (device code: ec_kernels_impl.h, instantiated per R in ec_kernels_inst.hip).
+#include <cstdlib>
+#include <type_traits>
 
-#include <algorithm>
+#include "ec_kernels_impl.h"
 
 namespace lsec {
 
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-template <int N> struct VecT;
-template <> struct VecT<1> { typedef uint32_t type; };
-template <> struct VecT<2> { typedef u32x2 type; };
-template <> struct VecT<4> { typedef u32x4 type; };
-
-constexpr int kBlock = 256;
-
-// The coefficient image is read-only and every lane of a wave reads the same cell, so read
-// it through the constant address space: uniform addresses there become s_load (SGPRs),
-// leaving the VALU and the vector memory pipe to the shard bytes.
-typedef const __attribute__((address_space(4))) CoefCell ConstCell;
-
-__device__ __forceinline__ ConstCell *const_cells(const CoefCell *p) {
-  return reinterpret_cast<ConstCell *>(reinterpret_cast<uintptr_t>(p));
-}
-
-// Shard addresses arrive as integers; give them the global address space explicitly so
-// loads/stores are global_* (vmcnt only) rather than flat_* (vmcnt + lgkmcnt).
-#define LSEC_GLOBAL __attribute__((address_space(1)))
-template <typename T>
-__device__ __forceinline__ const LSEC_GLOBAL T *gptr(uint64_t addr) {
-  return reinterpret_cast<const LSEC_GLOBAL T *>(addr);
-}
-template <typename T>
-__device__ __forceinline__ LSEC_GLOBAL T *gptr_w(uint64_t addr) {
-  return reinterpret_cast<LSEC_GLOBAL T *>(addr);
-}
-
-// ------------------------------------------------------------------ bytewise
-// one 32-bit word times constant (table cell), 4 bytes in parallel
-__device__ __forceinline__ uint32_t gf_mul_word(uint32_t ia, uint32_t ib, uint32_t ic,
-                                                const uint32_t (&t)[6]) {
-  return __builtin_amdgcn_perm(t[1], t[0], ia) ^ __builtin_amdgcn_perm(t[3], t[2], ib) ^
-         __builtin_amdgcn_perm(t[5], t[4], ic);
-}
-
-// Per-lane work unit of the bytewise kernel: 16 bytes (one dwordx4) per step, IT steps
-// 4 KiB apart per tile (tile = 256 * 16 * IT bytes of every shard).
-template <int IT>
-struct BwTile {
-  static constexpr int kBytes = kBlock * 16 * IT;
-};
-
-// Spread the grid so that each XCD (blocks b, b+8, b+16, ... are dealt to one XCD) gets a
-// contiguous run of tiles instead of every 8th tile: measured +2-3% HBM throughput on this
-// streaming pattern (tools/kprobe.hip).  Bijective for any grid size; placement is only a
-// speed hint, correctness never depends on it.
-__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
-  const uint32_t per = nb >> 3, rem = nb & 7, xcd = b & 7;
-  return xcd * per + min(xcd, rem) + (b >> 3);
-}
-
-template <int R, int kBwIt>
-__device__ __forceinline__ void bw_accumulate(u32x4 (&acc)[kBwIt][R], const u32x4 (&v)[kBwIt],
-                                              ConstCell *cells, int K, int j) {
-  u32x4 ia[kBwIt], ib[kBwIt], ic[kBwIt];
-#pragma unroll
-  for (int it = 0; it < kBwIt; ++it) {
-    ia[it] = v[it] & 0x07070707u;
-    ib[it] = (v[it] >> 3) & 0x07070707u;
-    ic[it] = (v[it] >> 6) & 0x03030303u;
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    ConstCell *cell = cells + r * K + j;  // wave-uniform -> scalar loads
-    const uint32_t c = cell->coef;
-    if (c == 0) continue;
-    if (c == 1) {
-#pragma unroll
-      for (int it = 0; it < kBwIt; ++it) acc[it][r] ^= v[it];
-      continue;
-    }
-    const uint32_t t[6] = {cell->ta_lo, cell->ta_hi, cell->tb_lo, cell->tb_hi, cell->tc_lo, cell->tc_hi};
-#pragma unroll
-    for (int it = 0; it < kBwIt; ++it)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc[it][r][e] ^= gf_mul_word(ia[it][e], ib[it][e], ic[it][e], t);
-  }
-}
-
-template <int R, int KC, int kBwIt>
-__global__ __launch_bounds__(kBlock) void k_gf8_bytewise(ApplyArgs a) {
-  constexpr int kBwTile = BwTile<kBwIt>::kBytes;
-  const int K = KC ? KC : a.K;
-  const int64_t C = a.size;
-  const uint32_t tiles_per_stripe = static_cast<uint32_t>((C + kBwTile - 1) / kBwTile);
-  const uint32_t ntiles = tiles_per_stripe * static_cast<uint32_t>(a.nstripes);
-  ConstCell *cells = const_cells(a.cells);
-
-  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
-    const uint32_t s = t / tiles_per_stripe;
-    const int64_t off0 = static_cast<int64_t>(t - s * tiles_per_stripe) * kBwTile + threadIdx.x * 16;
-    const bool full = (static_cast<int64_t>(t - s * tiles_per_stripe) + 1) * kBwTile <= C;  // wave-uniform
-
-    u32x4 acc[kBwIt][R];
-#pragma unroll
-    for (int it = 0; it < kBwIt; ++it)
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[it][r] = 0u;
-
-    if (full) {
-      if constexpr (KC > 0) {
-        // all K*IT loads in flight before any arithmetic
-        u32x4 v[KC][kBwIt];
-#pragma unroll
-        for (int j = 0; j < KC; ++j) {
-          const uint64_t p = a.in[j].base + s * a.in[j].stride + off0;
-#pragma unroll
-          for (int it = 0; it < kBwIt; ++it)
-            v[j][it] = __builtin_nontemporal_load(gptr<u32x4>(p + it * kBlock * 16));
-        }
-#pragma unroll
-        for (int j = 0; j < KC; ++j) bw_accumulate<R, kBwIt>(acc, v[j], cells, K, j);
-      } else {
-        for (int j0 = 0; j0 < K; j0 += 4) {
-          u32x4 v[4][kBwIt];
-          const int nj = min(4, K - j0);
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) {
-            if (jj < nj) {
-              const int j = j0 + jj;
-              const uint64_t p = a.in[j].base + s * a.in[j].stride + off0;
-#pragma unroll
-              for (int it = 0; it < kBwIt; ++it)
-                v[jj][it] = __builtin_nontemporal_load(gptr<u32x4>(p + it * kBlock * 16));
-            }
-          }
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj)
-            if (jj < nj) bw_accumulate<R, kBwIt>(acc, v[jj], cells, K, j0 + jj);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const uint64_t q = a.out[r].base + s * a.out[r].stride + off0;
-#pragma unroll
-        for (int it = 0; it < kBwIt; ++it)
-          __builtin_nontemporal_store(acc[it][r], gptr_w<u32x4>(q + it * kBlock * 16));
-      }
-    } else {
-      // ragged last tile: C is a multiple of 8, so each lane handles 16, 8 or 0 bytes per step
-      for (int j = 0; j < K; ++j) {
-        const uint64_t p = a.in[j].base + s * a.in[j].stride;
-        u32x4 v[kBwIt];
-#pragma unroll
-        for (int it = 0; it < kBwIt; ++it) {
-          const int64_t o = off0 + it * kBlock * 16;
-          v[it] = 0u;
-          if (o + 16 <= C) {
-            v[it] = *gptr<u32x4>(p + o);
-          } else if (o < C) {
-            const u32x2 h = *gptr<u32x2>(p + o);
-            v[it].x = h.x;
-            v[it].y = h.y;
-          }
-        }
-        bw_accumulate<R, kBwIt>(acc, v, cells, K, j);
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const uint64_t q = a.out[r].base + s * a.out[r].stride;
-#pragma unroll
-        for (int it = 0; it < kBwIt; ++it) {
-          const int64_t o = off0 + it * kBlock * 16;
-          if (o + 16 <= C) {
-            *gptr_w<u32x4>(q + o) = acc[it][r];
-          } else if (o < C) {
-            u32x2 h;
-            h.x = acc[it][r].x;
-            h.y = acc[it][r].y;
-            *gptr_w<u32x2>(q + o) = h;
-          }
-        }
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------ bitsliced
-// A lane owns DW consecutive dwords of packet-column space in one super-packet and reads
-// the same columns of all 8 packets of every input shard.
-template <int R, int KC, int DW>
-__global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
-  typedef typename VecT<DW>::type V;
-  const int K = KC ? KC : a.K;
-  const uint32_t P = static_cast<uint32_t>(a.packet);
-  const uint32_t col_bytes = static_cast<uint32_t>(a.size / 8);  // nsuper * P
-  constexpr uint32_t kTile = kBlock * 4 * DW;
-  const uint32_t tiles_per_stripe = (col_bytes + kTile - 1) / kTile;
-  const uint32_t ntiles = tiles_per_stripe * static_cast<uint32_t>(a.nstripes);
-  ConstCell *cells = const_cells(a.cells);
-
-  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
-    const uint32_t s = t / tiles_per_stripe;
-    const uint32_t colb = (t - s * tiles_per_stripe) * kTile + threadIdx.x * (4 * DW);
-    if (colb >= col_bytes) continue;  // only in a ragged last tile (P % 16 == 0 keeps a lane's DW dwords inside one packet)
-    const uint32_t sp = colb / P;
-    const int64_t off = static_cast<int64_t>(sp) * 8 * P + (colb - sp * P);
-
-    V acc[R][8];
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int x = 0; x < 8; ++x) acc[r][x] = 0u;
-
-    for (int j = 0; j < K; ++j) {
-      const uint64_t p = a.in[j].base + s * a.in[j].stride + off;
-      V e[8];
-#pragma unroll
-      for (int x = 0; x < 8; ++x) e[x] = __builtin_nontemporal_load(gptr<V>(p + x * P));
-      uint32_t c[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) c[r] = cells[r * K + j].coef;
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-          if ((c[r] >> b) & 1u) {
-#pragma unroll
-            for (int x = 0; x < 8; ++x) acc[r][x] ^= e[x];
-          }
-        if (b < 7) {  // e <- 2*e in bit-sliced form
-          const V top = e[7];
-          e[7] = e[6];
-          e[6] = e[5];
-          e[5] = e[4];
-          e[4] = e[3] ^ top;
-          e[3] = e[2] ^ top;
-          e[2] = e[1] ^ top;
-          e[1] = e[0];
-          e[0] = top;
-        }
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
-#pragma unroll
-      for (int x = 0; x < 8; ++x) __builtin_nontemporal_store(acc[r][x], gptr_w<V>(q + x * P));
-    }
-  }
-}
-
-// ------------------------------------------------------------------ host side
 namespace {
 
 int g_bw_variant = 0, g_bs_variant = 0;
@@ -289,52 +21,27 @@ int default_grid(uint64_t ntiles) {
   return static_cast<int>(std::min<uint64_t>(std::max<uint64_t>(ntiles, 1), cap));
 }
 
-template <int R, int IT>
-hipError_t bw_dispatch_k(const ApplyArgs &a, hipStream_t st, int grid) {
-  switch (a.K) {
-#define LSEC_BW_K(KK) \
-  case KK: hipLaunchKernelGGL((k_gf8_bytewise<R, KK, IT>), dim3(grid), dim3(kBlock), 0, st, a); break;
-    LSEC_BW_K(4) LSEC_BW_K(6) LSEC_BW_K(8) LSEC_BW_K(10) LSEC_BW_K(12) LSEC_BW_K(16) LSEC_BW_K(20)
-#undef LSEC_BW_K
-    default: hipLaunchKernelGGL((k_gf8_bytewise<R, 0, IT>), dim3(grid), dim3(kBlock), 0, st, a); break;
-  }
-  return hipGetLastError();
-}
-
-template <int IT>
-hipError_t bw_dispatch_r(const ApplyArgs &a, hipStream_t st, int grid) {
-  switch (a.R) {
-    case 1: return bw_dispatch_k<1, IT>(a, st, grid);
-    case 2: return bw_dispatch_k<2, IT>(a, st, grid);
-    case 3: return bw_dispatch_k<3, IT>(a, st, grid);
-    case 4: return bw_dispatch_k<4, IT>(a, st, grid);
-    case 5: return bw_dispatch_k<5, IT>(a, st, grid);
-    case 6: return bw_dispatch_k<6, IT>(a, st, grid);
-    case 7: return bw_dispatch_k<7, IT>(a, st, grid);
-    case 8: return bw_dispatch_k<8, IT>(a, st, grid);
+template <typename F>
+hipError_t by_r(int R, F f) {
+  switch (R) {
+    case 1: return f(std::integral_constant<int, 1>());
+    case 2: return f(std::integral_constant<int, 2>());
+    case 3: return f(std::integral_constant<int, 3>());
+    case 4: return f(std::integral_constant<int, 4>());
+    case 5: return f(std::integral_constant<int, 5>());
+    case 6: return f(std::integral_constant<int, 6>());
+    case 7: return f(std::integral_constant<int, 7>());
+    case 8: return f(std::integral_constant<int, 8>());
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int R, int DW>
-hipError_t bs_dispatch(const ApplyArgs &a, hipStream_t st, int grid) {
-  hipLaunchKernelGGL((k_gf8_bitsliced<R, 0, DW>), dim3(grid), dim3(kBlock), 0, st, a);
-  return hipGetLastError();
-}
-
-template <int DW>
-hipError_t bs_dispatch_r(const ApplyArgs &a, hipStream_t st, int grid) {
-  switch (a.R) {
-    case 1: return bs_dispatch<1, DW>(a, st, grid);
-    case 2: return bs_dispatch<2, DW>(a, st, grid);
-    case 3: return bs_dispatch<3, DW>(a, st, grid);
-    case 4: return bs_dispatch<4, DW>(a, st, grid);
-    case 5: return bs_dispatch<5, DW>(a, st, grid);
-    case 6: return bs_dispatch<6, DW>(a, st, grid);
-    case 7: return bs_dispatch<7, DW>(a, st, grid);
-    case 8: return bs_dispatch<8, DW>(a, st, grid);
-    default: return hipErrorInvalidValue;
-  }
+// (IT, MINW) shape for a K x R bytewise launch.  variant 0 = automatic policy, measured
+// (tools/kbench.py): two 4 KiB steps per lane while all K*IT loads of a lane fit the register
+// file at >= 2 waves/SIMD; the widest shapes (K*R >= 100, e.g. RS(20+6)) drop to one step.
+int bytewise_shape(int K, int R) {
+  if (g_bw_variant > 0) return g_bw_variant - 1;
+  return K * R >= 100 ? 1 : 0;
 }
 
 }  // namespace
@@ -347,12 +54,13 @@ void set_kernel_variant(int bw, int bs) {
 hipError_t launch_bytewise(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
   if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > 8 || a.size % 8 != 0) return hipErrorInvalidValue;
   if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
-  const int it = g_bw_variant == 1 ? 1 : 2;
+  const int shape = bytewise_shape(a.K, a.R);
+  const int it = (shape == 1 || shape == 3) ? 1 : 2;
   const uint64_t tile = static_cast<uint64_t>(kBlock) * 16 * it;
   const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);
-  return it == 1 ? bw_dispatch_r<1>(a, st, grid) : bw_dispatch_r<2>(a, st, grid);
+  return by_r(a.R, [&](auto r) { return dispatch_bytewise<decltype(r)::value>(a, st, grid, shape); });
 }
 
 hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
@@ -367,11 +75,7 @@ hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid_blocks)
   const uint64_t ntiles = ((col_bytes + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);
-  switch (dw) {
-    case 4: return bs_dispatch_r<4>(a, st, grid);
-    case 2: return bs_dispatch_r<2>(a, st, grid);
-    default: return bs_dispatch_r<1>(a, st, grid);
-  }
+  return by_r(a.R, [&](auto r) { return dispatch_bitsliced<decltype(r)::value>(a, st, grid, dw); });
 }
 
 }  // namespace lsec

@@ -241,3 +241,35 @@ def test_full_size_roundtrip_and_linearity(cuda):
         p.decode_dev(a, pa, [0], out=out)
         assert torch.equal(out[:, 0], a[:, 0])
     torch.cuda.synchronize()
+
+
+def test_host_path_many_batches(cuda):
+    """et_encode_stripes / et_decode_stripes across several staging batches (pipelined slots)."""
+    k, m, size, n = 6, 3, 1 << 20, 40   # 64 MiB staging -> 7 stripes per batch -> 6 batches
+    st = np.zeros((n, k + m, size), dtype=np.uint8)
+    rng = np.random.default_rng(3)
+    st[:, :k] = rng.integers(0, 256, (n, k, size), dtype=np.uint8)
+    with L.Plan.for_chunk(L.REED_SOL_VAN, k, m, size) as p:
+        p.encode_stripes(st)
+        for s in range(n):
+            assert np.array_equal(st[s, k:], O.encode(O.REED_SOL_VAN, st[s, :k], m)), s
+        keep = st[:, [1, k + 2]].copy()
+        st[:, [1, k + 2]] = 0
+        p.decode_stripes(st, [1, k + 2])
+        assert np.array_equal(st[:, [1, k + 2]], keep)
+
+
+@pytest.mark.parametrize("method,k,m,size", [(L.REED_SOL_VAN, 20, 6, 4 << 20), (L.CAUCHY_GOOD, 10, 4, 8 << 20)])
+def test_host_path_column_blocks(cuda, method, k, m, size):
+    """Stripes larger than half the staging budget are processed as column blocks."""
+    n = 2
+    st = np.zeros((n, k + m, size), dtype=np.uint8)
+    st[:, :k] = np.random.default_rng(k).integers(0, 256, (n, k, size), dtype=np.uint8)
+    with L.Plan.for_chunk(method, k, m, size) as p:
+        p.encode_stripes(st)
+        for s in range(n):
+            assert np.array_equal(st[s, k:], O.encode(method, st[s, :k], m, p.packet_size)), s
+        keep = st[:, [0, k - 1, k]].copy()
+        st[:, [0, k - 1, k]] = 7
+        p.decode_stripes(st, [0, k - 1, k])
+        assert np.array_equal(st[:, [0, k - 1, k]], keep)
