@@ -116,6 +116,19 @@ int lsec_encode_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int ns
 int lsec_decode_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int nstripes,
                     long long block_size, const int *erasures, void *stream);
 
+/* Per-stripe "magic": the 4-byte little-endian zlib adler32 over the concatenation of a
+ * stripe's k+m chunks that LStore's erasure segment stores in front of every chunk
+ * (je_cksum_calc, src/lio/segment/jerasure.c:169-182; checked by je_cksum_compare, :188-194).
+ * Computed on the GPU.  magic receives 4*nstripes bytes (host memory for et_*, device memory
+ * for lsec_*_dev).  The *_encode_* forms encode first and checksum data + fresh parity,
+ * which is what segjerase_write_func does per stripe (:1847-1850). */
+int et_encode_stripes_magic(lio_erasure_plan_t *plan, char **ptrs, int nstripes, int block_size, char *magic);
+int et_stripes_magic(lio_erasure_plan_t *plan, char **ptrs, int nstripes, int block_size, char *magic);
+int lsec_encode_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int nstripes,
+                          long long block_size, void *magic, void *stream);
+int lsec_stripe_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int nstripes,
+                          long long block_size, void *magic, void *stream);
+
 /* Pre-build (and cache on the current device) the decode matrix for one erasure pattern,
  * so the first lsec_decode_dev of that pattern does no host work.  0 / -1. */
 int lsec_prepare_decode(lio_erasure_plan_t *plan, const int *erasures);

@@ -589,9 +589,18 @@ size_t staging_budget() {
 // bytewise on any 8-byte boundary, bitsliced on super-packet boundaries -- so a block is a
 // valid independent sub-stripe).
 int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
-             const std::vector<int> &out_ids, const CoefCell *cells, int kind) {
+             const std::vector<int> &out_ids, const CoefCell *cells, int kind, uint8_t *magic_host = nullptr) {
   lio_erasure_plan_t *p = &e->pub;
   const int km = p->data_strips + p->parity_strips;
+  // staged position of every device id (for the stripe magic, which covers all k+m chunks)
+  std::vector<int> where(km, -1);  // >= 0: input slot j; <= -2: output slot (-2 - r)
+  for (size_t j = 0; j < in_ids.size(); ++j) where[in_ids[j]] = static_cast<int>(j);
+  for (size_t r = 0; r < out_ids.size(); ++r) where[out_ids[r]] = -2 - static_cast<int>(r);
+  if (magic_host) {
+    if (km > lsec::kMaxMagicShards) return fail("stripe magic supports at most %d chunks", lsec::kMaxMagicShards);
+    for (int i = 0; i < km; ++i)
+      if (where[i] == -1) return fail("stripe magic needs all %d chunks staged", km);
+  }
   const int nin = static_cast<int>(in_ids.size()), nout = static_cast<int>(out_ids.size());
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
@@ -610,6 +619,17 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   if (!stg) return fail("cannot create staging streams");
   int rc = 0;
   std::vector<CopyJob> jobs;
+  unsigned long long *dacc = nullptr;
+  uint8_t *dmagic = nullptr;
+  if (magic_host) {
+    hipError_t err = hipMallocAsync(reinterpret_cast<void **>(&dacc), 16ull * nstripes + 4ull * nstripes, stg->s_out);
+    if (err == hipSuccess) err = hipMemsetAsync(dacc, 0, 16ull * nstripes, stg->s_out);
+    if (err != hipSuccess) {
+      delete stg;
+      return fail("magic workspace: %s", hipGetErrorString(err));
+    }
+    dmagic = reinterpret_cast<uint8_t *>(dacc + 2ull * nstripes);
+  }
 
   auto unpack = [&](Staging::Slot &sl) -> int {
     if (!sl.pending) return 0;
@@ -652,8 +672,21 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
         in[j] = {reinterpret_cast<uint64_t>(sl.d) + static_cast<uint64_t>(j) * len, static_cast<int64_t>(nin * len)};
       for (int r = 0; r < nout; ++r)
         out[r] = {reinterpret_cast<uint64_t>(sl.d) + out_off + static_cast<uint64_t>(r) * len, static_cast<int64_t>(nout * len)};
-      if ((rc = enqueue_apply(kind, cells, nin, nout, in, out, nb, clen, p->packet_size, stg->s_out))) break;
-      err = hipMemcpyAsync(sl.h + out_off, sl.d + out_off, static_cast<size_t>(nb) * nout * len, hipMemcpyDeviceToHost, stg->s_out);
+      if (nout > 0 && (rc = enqueue_apply(kind, cells, nin, nout, in, out, nb, clen, p->packet_size, stg->s_out))) break;
+      if (magic_host) {
+        lsec::MagicArgs ma;
+        std::memset(&ma, 0, sizeof(ma));
+        ma.nshards = km;
+        ma.nstripes = nb;
+        ma.size = clen;
+        ma.col0 = c0;
+        ma.chunk = C;
+        ma.acc = dacc + 2ull * s0;
+        for (int i = 0; i < km; ++i) ma.sh[i] = where[i] >= 0 ? in[where[i]] : out[-2 - where[i]];
+        err = lsec::launch_stripe_magic(ma, stg->s_out);
+        if (err != hipSuccess) { rc = fail("magic launch: %s", hipGetErrorString(err)); break; }
+      }
+      if (nout > 0) err = hipMemcpyAsync(sl.h + out_off, sl.d + out_off, static_cast<size_t>(nb) * nout * len, hipMemcpyDeviceToHost, stg->s_out);
       if (err == hipSuccess) err = hipEventRecord(sl.done, stg->s_out);
       if (err != hipSuccess) { rc = fail("D2H: %s", hipGetErrorString(err)); break; }
       sl.pending = true;
@@ -664,10 +697,19 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
       sl.clen = clen;
     }
   }
+  if (magic_host && rc == 0) {
+    hipError_t err = lsec::launch_magic_finalize(dacc, nstripes, static_cast<int64_t>(km) * C, dmagic, stg->s_out);
+    if (err == hipSuccess) err = hipMemcpyAsync(magic_host, dmagic, 4ull * nstripes, hipMemcpyDeviceToHost, stg->s_out);
+    if (err != hipSuccess) rc = fail("magic finalize: %s", hipGetErrorString(err));
+  }
   // drain in submission order
   for (int i = 0; i < kSlots; ++i) {
     const int r2 = unpack(stg->slot[(which + i) % kSlots]);
     if (!rc) rc = r2;
+  }
+  if (dacc) {
+    if (hipStreamSynchronize(stg->s_out) != hipSuccess && !rc) rc = fail("magic sync failed");
+    (void)hipFreeAsync(dacc, stg->s_out);
   }
   if (rc) {
     (void)hipStreamSynchronize(stg->s_in);
@@ -763,6 +805,61 @@ int decode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C, cons
   CoefCell *cells = nullptr;
   if (decode_entry(e, ids, &ent, &cells)) return -1;
   return run_host(e, ptrs, nstripes, C, ent->dp.survivors, ent->dp.erased, cells, kernel_kind(p->method, p->w));
+}
+
+int encode_stripes_magic_impl(PlanExt *e, char **ptrs, int nstripes, long long C, uint8_t *magic) {
+  lio_erasure_plan_t *p = &e->pub;
+  if (!ptrs || !magic) return fail("ptrs / magic is NULL");
+  if (check_geometry(p, C)) return -1;
+  if (nstripes <= 0 || C == 0) return 0;
+  CoefCell *cells = nullptr;
+  if (encode_cells(e, &cells)) return -1;
+  const int k = p->data_strips;
+  const int R = static_cast<int>(e->impl->coding.size()) / k;
+  if (R != p->parity_strips) return fail("stripe magic needs m parity rows");
+  std::vector<int> in_ids(k), out_ids(R);
+  for (int j = 0; j < k; ++j) in_ids[j] = j;
+  for (int r = 0; r < R; ++r) out_ids[r] = k + r;
+  return run_host(e, ptrs, nstripes, C, in_ids, out_ids, cells, kernel_kind(p->method, p->w), magic);
+}
+
+int stripes_magic_impl(PlanExt *e, char **ptrs, int nstripes, long long C, uint8_t *magic) {
+  lio_erasure_plan_t *p = &e->pub;
+  if (!ptrs || !magic) return fail("ptrs / magic is NULL");
+  if (C < 0 || C % 8 != 0) return fail("block_size %lld is not a multiple of 8", C);
+  if (nstripes <= 0 || C == 0) return 0;
+  const int km = p->data_strips + p->parity_strips;
+  std::vector<int> in_ids(km), none;
+  for (int i = 0; i < km; ++i) in_ids[i] = i;
+  return run_host(e, ptrs, nstripes, C, in_ids, none, nullptr, KBYTEWISE, magic);
+}
+
+int magic_dev_impl(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C, uint8_t *magic, hipStream_t st) {
+  lio_erasure_plan_t *p = &e->pub;
+  const int km = p->data_strips + p->parity_strips;
+  if (km > lsec::kMaxMagicShards) return fail("stripe magic supports at most %d chunks", lsec::kMaxMagicShards);
+  if (C < 0 || C % 8 != 0) return fail("block_size %lld is not a multiple of 8", C);
+  if (nstripes <= 0 || C == 0) return 0;
+  unsigned long long *acc = nullptr;
+  HIP_OK(hipMallocAsync(reinterpret_cast<void **>(&acc), 16ull * nstripes, st));
+  HIP_OK(hipMemsetAsync(acc, 0, 16ull * nstripes, st));
+  lsec::MagicArgs ma;
+  std::memset(&ma, 0, sizeof(ma));
+  ma.nshards = km;
+  ma.size = C;
+  ma.col0 = 0;
+  ma.chunk = C;
+  const int per = static_cast<int>(std::max(1LL, (1LL << 30) / std::max(1LL, C / 8192 + 1)));
+  for (int s0 = 0; s0 < nstripes; s0 += per) {
+    ma.nstripes = std::min(per, nstripes - s0);
+    ma.acc = acc + 2ull * s0;
+    for (int i = 0; i < km; ++i)
+      ma.sh[i] = {reinterpret_cast<uint64_t>(sh[i].base) + static_cast<uint64_t>(s0) * sh[i].stride, sh[i].stride};
+    HIP_OK(lsec::launch_stripe_magic(ma, st));
+  }
+  HIP_OK(lsec::launch_magic_finalize(acc, nstripes, static_cast<int64_t>(km) * C, magic, st));
+  HIP_OK(hipFreeAsync(acc, st));
+  return 0;
 }
 
 // plan->encode_block / plan->decode_block
@@ -1106,6 +1203,35 @@ int lsec_decode_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int ns
   if (!e) return fail("not an lstore_ec plan");
   if (!shards) return fail("shards is NULL");
   return decode_dev(e, shards, nstripes, block_size, erasures, static_cast<hipStream_t>(stream));
+}
+
+int et_encode_stripes_magic(lio_erasure_plan_t *plan, char **ptrs, int nstripes, int block_size, char *magic) {
+  PlanExt *e = ext_of(plan);
+  if (!e) return fail("not an lstore_ec plan");
+  return encode_stripes_magic_impl(e, ptrs, nstripes, block_size, reinterpret_cast<uint8_t *>(magic));
+}
+
+int et_stripes_magic(lio_erasure_plan_t *plan, char **ptrs, int nstripes, int block_size, char *magic) {
+  PlanExt *e = ext_of(plan);
+  if (!e) return fail("not an lstore_ec plan");
+  return stripes_magic_impl(e, ptrs, nstripes, block_size, reinterpret_cast<uint8_t *>(magic));
+}
+
+int lsec_stripe_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int nstripes, long long block_size,
+                          void *magic, void *stream) {
+  PlanExt *e = ext_of(plan);
+  if (!e) return fail("not an lstore_ec plan");
+  if (!shards || !magic) return fail("shards / magic is NULL");
+  return magic_dev_impl(e, shards, nstripes, block_size, static_cast<uint8_t *>(magic), static_cast<hipStream_t>(stream));
+}
+
+int lsec_encode_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int nstripes, long long block_size,
+                          void *magic, void *stream) {
+  PlanExt *e = ext_of(plan);
+  if (!e) return fail("not an lstore_ec plan");
+  if (!shards || !magic) return fail("shards / magic is NULL");
+  if (encode_dev(e, shards, nstripes, block_size, static_cast<hipStream_t>(stream))) return -1;
+  return magic_dev_impl(e, shards, nstripes, block_size, static_cast<uint8_t *>(magic), static_cast<hipStream_t>(stream));
 }
 
 int lsec_prepare_decode(lio_erasure_plan_t *plan, const int *erasures) {

@@ -52,6 +52,31 @@ struct ApplyArgs {
   ShardRef out[kMaxR];
 };
 
+// Per-stripe adler32 "magic" of LStore's erasure segment (je_cksum_calc,
+// src/lio/segment/jerasure.c:169-182): zlib adler32 (RFC 1950) over the concatenation of all
+// k+m chunks of a stripe, stored as 4 little-endian bytes.  Computed with position-weighted
+// partial sums: over bytes b_i at positions i of a stream of length L,
+//   A = 1 + sum b_i,  B = L + sum (L - i) b_i   (mod 65521)
+// so any tile of any shard contributes independently (S = sum b, U = sum (i - p0) b via
+// v_dot4_u32_u8), blocks add their reduced partials into 2 x u64 per stripe (acc), and a
+// finalize kernel folds them into the magic.
+constexpr int kMaxMagicShards = kMaxK + kMaxR;
+
+struct MagicArgs {
+  int nshards;            // shards per stripe, in checksum order (LStore: data 0..k-1, parity 0..m-1)
+  int nstripes;
+  int64_t size;           // bytes of each shard covered by this launch
+  int64_t col0;           // column offset of those bytes inside the chunk (column-block staging)
+  int64_t chunk;          // full chunk size C (checksum positions are i*C + col0 + o)
+  unsigned long long *acc;  // 2 per stripe: sum A, sum B (zeroed before the first launch)
+  ShardRef sh[kMaxMagicShards];
+};
+
+hipError_t launch_stripe_magic(const MagicArgs &a, hipStream_t stream);
+// magic[s*4 .. s*4+3] from acc (total_len = shards * C)
+hipError_t launch_magic_finalize(const unsigned long long *acc, int nstripes, int64_t total_len, uint8_t *magic,
+                                 hipStream_t stream);
+
 // Host helper: fill one cell for coefficient c.
 void make_cell(uint8_t c, CoefCell &cell);
 

@@ -78,4 +78,104 @@ hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid_blocks)
   return by_r(a.R, [&](auto r) { return dispatch_bitsliced<decltype(r)::value>(a, st, grid, dw); });
 }
 
+// ------------------------------------------------------------------ stripe magic (adler32)
+namespace {
+
+constexpr uint32_t kAdlerMod = 65521;
+
+__device__ __forceinline__ void adler_add16(u32x4 v, uint64_t len_minus_pos, uint64_t &a_sum, uint64_t &b_sum) {
+  // S = sum of the 16 bytes, U = sum t*b_t (t = 0..15) via packed byte dot products
+  uint32_t S = 0, U = 0;
+  S = __builtin_amdgcn_udot4(v.x, 0x01010101u, S, false);
+  S = __builtin_amdgcn_udot4(v.y, 0x01010101u, S, false);
+  S = __builtin_amdgcn_udot4(v.z, 0x01010101u, S, false);
+  S = __builtin_amdgcn_udot4(v.w, 0x01010101u, S, false);
+  U = __builtin_amdgcn_udot4(v.x, 0x03020100u, U, false);
+  U = __builtin_amdgcn_udot4(v.y, 0x07060504u, U, false);
+  U = __builtin_amdgcn_udot4(v.z, 0x0B0A0908u, U, false);
+  U = __builtin_amdgcn_udot4(v.w, 0x0F0E0D0Cu, U, false);
+  a_sum += S;
+  b_sum += len_minus_pos * S - U;   // sum_t (L - p - t) b_t, every term >= 0
+}
+
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *lds) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < kBlock / 64; ++w) t += lds[w];
+  __syncthreads();
+  return t;
+}
+
+// one block per (stripe, 8 KiB column tile); each lane reads 16 B x 2 of every shard
+__global__ __launch_bounds__(kBlock) void k_stripe_magic(MagicArgs a) {
+  __shared__ uint32_t red[kBlock / 64];
+  constexpr int kIt = 2, kTile = kBlock * 16 * kIt;
+  const int64_t C = a.size;
+  const uint32_t tps = static_cast<uint32_t>((C + kTile - 1) / kTile);
+  const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
+  const uint64_t L = static_cast<uint64_t>(a.nshards) * a.chunk;
+  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+    const uint32_t s = t / tps;
+    const int64_t off0 = static_cast<int64_t>(t - s * tps) * kTile + threadIdx.x * 16;
+    uint64_t as = 0, bs = 0;
+    for (int i = 0; i < a.nshards; ++i) {
+      const uint64_t base = a.sh[i].base + s * a.sh[i].stride;
+#pragma unroll
+      for (int it = 0; it < kIt; ++it) {
+        const int64_t o = off0 + it * kBlock * 16;
+        u32x4 v = 0u;
+        if (o + 16 <= C) {
+          v = __builtin_nontemporal_load(gptr<u32x4>(base + o));
+        } else if (o < C) {
+          const u32x2 h = *gptr<u32x2>(base + o);
+          v.x = h.x;
+          v.y = h.y;
+        }
+        adler_add16(v, L - static_cast<uint64_t>(i * a.chunk + a.col0 + o), as, bs);
+      }
+    }
+    const uint32_t am = block_sum(static_cast<uint32_t>(as % kAdlerMod), red);
+    const uint32_t bm = block_sum(static_cast<uint32_t>(bs % kAdlerMod), red);
+    if (threadIdx.x == 0) {
+      atomicAdd(a.acc + 2 * s, static_cast<unsigned long long>(am));
+      atomicAdd(a.acc + 2 * s + 1, static_cast<unsigned long long>(bm));
+    }
+  }
+}
+
+__global__ void k_magic_finalize(const unsigned long long *acc, int nstripes, uint64_t total_len, uint8_t *magic) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nstripes) return;
+  const uint32_t A = static_cast<uint32_t>((1 + acc[2 * s]) % kAdlerMod);
+  const uint32_t B = static_cast<uint32_t>((total_len % kAdlerMod + acc[2 * s + 1]) % kAdlerMod);
+  const uint32_t m = (B << 16) | A;
+  magic[4 * s + 0] = m & 255;
+  magic[4 * s + 1] = (m >> 8) & 255;
+  magic[4 * s + 2] = (m >> 16) & 255;
+  magic[4 * s + 3] = m >> 24;
+}
+
+}  // namespace
+
+hipError_t launch_stripe_magic(const MagicArgs &a, hipStream_t st) {
+  if (a.nshards < 1 || a.nshards > kMaxMagicShards || a.size % 8 != 0) return hipErrorInvalidValue;
+  if (a.nstripes <= 0) return hipSuccess;
+  const uint64_t tile = kBlock * 16 * 2;
+  const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
+  if (ntiles >= (1ull << 31) || a.size == 0) return a.size == 0 ? hipSuccess : hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_stripe_magic, dim3(default_grid(ntiles)), dim3(kBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_magic_finalize(const unsigned long long *acc, int nstripes, int64_t total_len, uint8_t *magic,
+                                 hipStream_t st) {
+  if (nstripes <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_magic_finalize, dim3((nstripes + 255) / 256), dim3(256), 0, st, acc, nstripes,
+                     static_cast<uint64_t>(total_len), magic);
+  return hipGetLastError();
+}
+
 }  // namespace lsec

@@ -70,7 +70,8 @@ class ShardRef(C.Structure):
 # every function include/lstore_ec.h declares (tests check the .so exports all of them)
 EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan", "et_destroy_plan",
            "et_encode", "et_decode", "et_encode_stripes", "et_decode_stripes", "lsec_encode_dev",
-           "lsec_decode_dev", "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count",
+           "lsec_decode_dev", "et_encode_stripes_magic", "et_stripes_magic", "lsec_encode_magic_dev",
+           "lsec_stripe_magic_dev", "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count",
            "lsec_last_error", "lsec_plan_kernel", "lsec_set_kernel_variant")
 
 _lib = None
@@ -114,6 +115,10 @@ def lib():
     L.lsec_encode_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.c_void_p]
     L.lsec_decode_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.POINTER(C.c_int), C.c_void_p]
     L.lsec_prepare_decode.argtypes = [P, C.POINTER(C.c_int)]
+    L.et_encode_stripes_magic.argtypes = [P, C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_void_p]
+    L.et_stripes_magic.argtypes = [P, C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_void_p]
+    L.lsec_encode_magic_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.c_void_p, C.c_void_p]
+    L.lsec_stripe_magic_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.c_void_p, C.c_void_p]
     L.lsec_last_error.restype = C.c_char_p
     L.lsec_plan_kernel.argtypes = [P]
     L.lsec_set_kernel_variant.argtypes = [C.c_int, C.c_int]
@@ -283,6 +288,31 @@ class Plan:
     def decode_stripes_ptrs(self, ptr_array, nstripes: int, block_size: int, erasures) -> None:
         _check(lib().et_decode_stripes(self._p, ptr_array, nstripes, block_size, _erasure_array(erasures)),
                "et_decode_stripes")
+
+    # -- stripe magic (je_cksum_calc, segment/jerasure.c:169-182)
+    def encode_stripes_magic(self, stripes: np.ndarray) -> np.ndarray:
+        """Encode + per-stripe 4-byte adler32 magic over all k+m chunks; returns uint8 [N, 4]."""
+        arr, n, size = self._stripe_ptrs(stripes)
+        magic = np.zeros((n, 4), dtype=np.uint8)
+        _check(lib().et_encode_stripes_magic(self._p, arr, n, size, magic.ctypes.data), "et_encode_stripes_magic")
+        return magic
+
+    def stripes_magic(self, stripes: np.ndarray) -> np.ndarray:
+        arr, n, size = self._stripe_ptrs(stripes)
+        magic = np.zeros((n, 4), dtype=np.uint8)
+        _check(lib().et_stripes_magic(self._p, arr, n, size, magic.ctypes.data), "et_stripes_magic")
+        return magic
+
+    def encode_magic_dev(self, data, parity, magic, stream=None) -> None:
+        """torch: encode + magic (uint8 [N,4] device tensor)."""
+        refs, n, size = self.tensor_refs(data, parity)
+        _check(lib().lsec_encode_magic_dev(self._p, self.shard_refs(refs), n, size, magic.data_ptr(),
+                                           _stream_handle(stream)), "lsec_encode_magic_dev")
+
+    def stripe_magic_dev(self, data, parity, magic, stream=None) -> None:
+        refs, n, size = self.tensor_refs(data, parity)
+        _check(lib().lsec_stripe_magic_dev(self._p, self.shard_refs(refs), n, size, magic.data_ptr(),
+                                           _stream_handle(stream)), "lsec_stripe_magic_dev")
 
     # -- device-resident calls
     @staticmethod

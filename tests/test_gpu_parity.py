@@ -273,3 +273,35 @@ def test_host_path_column_blocks(cuda, method, k, m, size):
         st[:, [0, k - 1, k]] = 7
         p.decode_stripes(st, [0, k - 1, k])
         assert np.array_equal(st[:, [0, k - 1, k]], keep)
+
+
+# ---------------------------------------------------------------- stripe magic (adler32, segment/jerasure.c:169-182)
+def _je_magic(full):
+    """je_cksum_calc: adler32 over the k+m chunks in order, 4 bytes little-endian (zlib)."""
+    a = 1
+    for row in full:
+        a = zlib.adler32(row.tobytes(), a)
+    return np.frombuffer(np.uint32(a).tobytes(), dtype=np.uint8)
+
+
+@pytest.mark.parametrize("method,k,m,size", [(L.REED_SOL_VAN, 6, 3, 65536), (L.CAUCHY_GOOD, 10, 4, 1 << 20),
+                                             (L.REED_SOL_VAN, 6, 3, 8200), (L.REED_SOL_VAN, 20, 6, 4 << 20)])
+def test_stripe_magic_matches_zlib(cuda, method, k, m, size):
+    import torch
+
+    n = 5
+    st = np.zeros((n, k + m, size), dtype=np.uint8)
+    st[:, :k] = np.random.default_rng(size % 977).integers(0, 256, (n, k, size), dtype=np.uint8)
+    st[1, :k] = 0xFF  # worst case for the modular sums
+    with L.Plan.for_chunk(method, k, m, size) as p:
+        magic = p.encode_stripes_magic(st)          # host path: GPU encode + GPU magic
+        for s in range(n):
+            assert np.array_equal(st[s, k:], O.encode(method, st[s, :k], m, p.packet_size))
+            assert np.array_equal(magic[s], _je_magic(st[s])), s
+        assert np.array_equal(p.stripes_magic(st), magic)
+        d = torch.from_numpy(st[:, :k].copy()).to(cuda)
+        par = torch.zeros((n, m, size), dtype=torch.uint8, device=cuda)
+        mg = torch.zeros((n, 4), dtype=torch.uint8, device=cuda)
+        p.encode_magic_dev(d, par, mg)
+        torch.cuda.synchronize()
+        assert np.array_equal(mg.cpu().numpy(), magic)
