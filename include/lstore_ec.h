@@ -129,6 +129,17 @@ int lsec_encode_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, 
 int lsec_stripe_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int nstripes,
                           long long block_size, void *magic, void *stream);
 
+/* Batched write side of LStore's erasure segment (segjerase_write_func,
+ * src/lio/segment/jerasure.c:1640-1895, for whole-stripe-aligned writes) including the LUN
+ * child's placement (lun_row_decompose, src/lio/segment/lun.c:1140-1246).
+ * data: nstripes*k*C user bytes (host memory, stripe-major, as the cache page holds them).
+ * dev[i] (i = 0..k+m-1, host memory, nstripes*(C+4) bytes each) receives, at offset
+ * s*(C+4), the LUN chunk [4-byte stripe magic | chunk j] with
+ * j = (i + (first_stripe + s)*n_shift) % (k+m) -- data chunk j for j < k, parity j-k else.
+ * Parity and magics are computed on the GPU.  0 / -1. */
+int lsec_segment_write(lio_erasure_plan_t *plan, const char *data, int nstripes, int chunk, int n_shift,
+                       long long first_stripe, char **dev);
+
 /* Pre-build (and cache on the current device) the decode matrix for one erasure pattern,
  * so the first lsec_decode_dev of that pattern does no host work.  0 / -1. */
 int lsec_prepare_decode(lio_erasure_plan_t *plan, const int *erasures);

@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "../../include/lstore_ec.h"
+#include "ec_host.h"
 #include "ec_kernels.h"
 #include "gf8.h"
 
@@ -886,6 +887,13 @@ int fp_dummy(lio_erasure_plan_t *) { return 0; }
 }  // namespace
 
 namespace lsec {
+
+void parallel_copy(std::vector<HostCopy> &jobs) {
+  std::vector<CopyJob> j;
+  j.reserve(jobs.size());
+  for (const HostCopy &h : jobs) j.push_back({h.dst, h.src, h.bytes});
+  CopyPool::get().run(j);
+}
 
 void make_cell(uint8_t c, CoefCell &cell) {
   uint8_t ta[8], tb[8], tc[8] = {0, 0, 0, 0, 0, 0, 0, 0};

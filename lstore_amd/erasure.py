@@ -71,7 +71,7 @@ class ShardRef(C.Structure):
 EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan", "et_destroy_plan",
            "et_encode", "et_decode", "et_encode_stripes", "et_decode_stripes", "lsec_encode_dev",
            "lsec_decode_dev", "et_encode_stripes_magic", "et_stripes_magic", "lsec_encode_magic_dev",
-           "lsec_stripe_magic_dev", "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count",
+           "lsec_stripe_magic_dev", "lsec_segment_write", "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count",
            "lsec_last_error", "lsec_plan_kernel", "lsec_set_kernel_variant")
 
 _lib = None
@@ -119,6 +119,7 @@ def lib():
     L.et_stripes_magic.argtypes = [P, C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_void_p]
     L.lsec_encode_magic_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.c_void_p, C.c_void_p]
     L.lsec_stripe_magic_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.c_void_p, C.c_void_p]
+    L.lsec_segment_write.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_void_p]
     L.lsec_last_error.restype = C.c_char_p
     L.lsec_plan_kernel.argtypes = [P]
     L.lsec_set_kernel_variant.argtypes = [C.c_int, C.c_int]
@@ -313,6 +314,18 @@ class Plan:
         refs, n, size = self.tensor_refs(data, parity)
         _check(lib().lsec_stripe_magic_dev(self._p, self.shard_refs(refs), n, size, magic.data_ptr(),
                                            _stream_handle(stream)), "lsec_stripe_magic_dev")
+
+    # -- segment adapter (segjerase_write_func + LUN placement)
+    def segment_write(self, data: np.ndarray, n_shift: int = 1, first_stripe: int = 0) -> np.ndarray:
+        """data uint8 [N, k, C] -> device images uint8 [k+m, N*(C+4)] (lsec_segment_write)."""
+        n_str, k, size = data.shape
+        n = self.k + self.m
+        data = np.ascontiguousarray(data)
+        dev = np.zeros((n, n_str * (size + 4)), dtype=np.uint8)
+        ptrs = self._ptr_array([dev[i].ctypes.data for i in range(n)])
+        _check(lib().lsec_segment_write(self._p, data.ctypes.data, n_str, size, n_shift, first_stripe, ptrs),
+               "lsec_segment_write")
+        return dev
 
     # -- device-resident calls
     @staticmethod

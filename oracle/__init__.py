@@ -80,6 +80,9 @@ def ref():
         lib.ref_plan_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
         lib.ref_plan_encode_many.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
         lib.ref_plan_decode_many.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        lib.ref_segment_write.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong,
+                                          C.c_void_p]
+        lib.ref_segment_write.restype = None
         _ref = lib
     return _ref
 
@@ -208,6 +211,16 @@ class RefPlan:
         km, size = shards.shape
         return self.lib.ref_plan_decode(self.h, _ptrs([shards[i] for i in range(km)]), size,
                                         _iarr(list(erasures) + [-1]))
+
+    def segment_write(self, data, nstripes, chunk, n_shift=1, first_stripe=0):
+        """segjerase_write_func + LUN placement restated over the real jerasure (config c1).
+        data: uint8 [nstripes, k, C]; returns uint8 [k+m, nstripes*(C+4)] device images."""
+        n = self.k + self.m
+        dev = np.zeros((n, nstripes * (chunk + 4)), dtype=np.uint8)
+        ptrs = _ptrs([dev[i] for i in range(n)])
+        data = np.ascontiguousarray(data)
+        self.lib.ref_segment_write(self.h, data.ctypes.data, nstripes, chunk, n_shift, first_stripe, ptrs)
+        return dev
 
     def encode_many(self, ptr_array, nstripes, size, nthreads):
         return self.lib.ref_plan_encode_many(self.h, ptr_array, nstripes, size, nthreads)

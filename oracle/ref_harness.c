@@ -24,6 +24,7 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <zlib.h>
 
 #include "jerasure.h"
 #include "galois.h"
@@ -223,4 +224,39 @@ int ref_plan_decode_many(ref_plan_t *p, char **ptrs, int nstripes, int size, int
                          int *erasures)
 {
     return ref_many(p, ptrs, nstripes, size, nthreads, 1, erasures);
+}
+
+/* ---- config c1 plumbing: the per-stripe work of segjerase_write_func for a whole-stripe
+ * aligned write (src/lio/segment/jerasure.c:1782-1855), restated without gop/tbx/IBP:
+ *   ptr[0..k) -> user data, ptr[k..k+m) -> parity buffer   (:1809-1844)
+ *   plan->encode_block(plan, ptr, C)                        (:1847)  -- real jerasure
+ *   je_cksum_calc(magic, ptr, k+m, C): zlib adler32 over the k+m chunks, 4 bytes LE (:169-182)
+ * and the LUN child's placement of the 2(k+m) [magic | chunk] iovecs: physical device i
+ * stores logical chunk (i + s*n_shift) % (k+m) of stripe s at offset s*(C+4)
+ * (lun_row_decompose, lun.c:1140-1246).  dev[i] holds nstripes*(C+4) bytes. */
+void ref_segment_write(ref_plan_t *p, const char *data, int nstripes, int chunk, int n_shift,
+                       long long first_stripe, char **dev)
+{
+    int k = p->k, m = p->m, n = k + m;
+    size_t C = (size_t)chunk, lchunk = C + 4;
+    char **ptr = (char **)malloc(sizeof(char *) * n);
+    char *parity = (char *)malloc(C * m);
+    for (int s = 0; s < nstripes; s++) {
+        for (int j = 0; j < k; j++) ptr[j] = (char *)data + ((size_t)s * k + j) * C;
+        for (int r = 0; r < m; r++) ptr[k + r] = parity + (size_t)r * C;
+        ref_plan_encode(p, ptr, chunk);
+        unsigned long ck = adler32(0L, Z_NULL, 0);
+        for (int i = 0; i < n; i++) ck = adler32(ck, (unsigned char *)ptr[i], chunk);
+        unsigned char magic[4];
+        for (int i = 0; i < 4; i++) { magic[i] = ck & 255; ck >>= 8; }
+        long long ss = first_stripe + s;
+        for (int i = 0; i < n; i++) {
+            int j = (int)((i + ss * n_shift) % n);
+            char *slot = dev[i] + (size_t)s * lchunk;
+            memcpy(slot, magic, 4);
+            memcpy(slot + 4, ptr[j], C);
+        }
+    }
+    free(parity);
+    free(ptr);
 }

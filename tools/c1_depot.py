@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""BASELINE config c1: RS(6+3) encode of 1000 x 64 KiB stripes through the segment write path.
+
+The reference's c1 runs src/lio over vendor/jerasure into loopback IBP depots.  IBP
+(APR/ZMQ/leveldb) cannot be built offline, so the depots are files:
+  reference  oracle/_ref ref_segment_write: segjerase_write_func's per-stripe loop restated
+             over the real jerasure encode_block + zlib adler32 magic + LUN placement
+  engine     lsec_segment_write: one call, parity + magic on the GPU
+Both produce k+m device images; they must be byte-identical.  Rates are user-data GiB/s,
+with and without writing the images to depot files (--depot-dir, default /tmp).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def write_depots(dev, dirname, tag):
+    t0 = time.perf_counter()
+    for i in range(dev.shape[0]):
+        with open(os.path.join(dirname, f"{tag}_depot{i}.bin"), "wb") as f:
+            f.write(dev[i].tobytes())
+            f.flush()
+            os.fsync(f.fileno())
+    return time.perf_counter() - t0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stripes", type=int, default=1000)
+    ap.add_argument("--chunk", type=int, default=64 << 10)
+    ap.add_argument("--k", type=int, default=6)
+    ap.add_argument("--m", type=int, default=3)
+    ap.add_argument("--method", default="reed_sol_van")
+    ap.add_argument("--n-shift", type=int, default=1)
+    ap.add_argument("--depot-dir", default="/tmp")
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+
+    import lstore_amd as L
+    import oracle as O
+    from lstore_amd import erasure as E
+
+    meth = E.JE_METHOD_NAMES.index(a.method)
+    k, m, C, N = a.k, a.m, a.chunk, a.stripes
+    rng = np.random.default_rng(0x4C53544F5245)
+    data = rng.integers(0, 256, (N, k, C), dtype=np.uint8)
+    gib = k * C * N / 2**30
+
+    plan = L.Plan.for_chunk(meth, k, m, C)
+    rp = O.RefPlan(meth, k, m, 8, plan.packet_size)
+
+    plan.segment_write(data[:2], a.n_shift, 0)  # warm staging / device images
+    t_ref, t_eng = [], []
+    for _ in range(a.reps):
+        t0 = time.perf_counter()
+        ref = rp.segment_write(data, N, C, a.n_shift, 0)
+        t_ref.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        ours = plan.segment_write(data, a.n_shift, 0)
+        t_eng.append(time.perf_counter() - t0)
+    identical = bool(np.array_equal(ref, ours))
+    t_io_ref = write_depots(ref, a.depot_dir, "c1ref")
+    t_io_eng = write_depots(ours, a.depot_dir, "c1eng")
+    for tag in ("c1ref", "c1eng"):
+        for i in range(k + m):
+            os.remove(os.path.join(a.depot_dir, f"{tag}_depot{i}.bin"))
+    tr, te = min(t_ref), min(t_eng)
+    print(json.dumps({
+        "config": "c1", "workload": f"{a.method}({k}+{m}) segment write, {N} stripes x C={C} B, n_shift={a.n_shift}",
+        "images_identical": identical,
+        "reference_cpu_gibps": round(gib / tr, 3), "reference_cores": 1,
+        "engine_gibps": round(gib / te, 3),
+        "reference_with_depot_files_gibps": round(gib / (tr + t_io_ref), 3),
+        "engine_with_depot_files_gibps": round(gib / (te + t_io_eng), 3),
+        "depot_dir": a.depot_dir,
+        "note": "reference = segjerase_write_func loop over real jerasure + zlib (oracle/_ref); engine = "
+                "lsec_segment_write (GPU parity + magic, host memory in/out, PCIe included)",
+    }), flush=True)
+    if not identical:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()
