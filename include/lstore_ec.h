@@ -140,6 +140,18 @@ int lsec_stripe_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, 
 int lsec_segment_write(lio_erasure_plan_t *plan, const char *data, int nstripes, int chunk, int n_shift,
                        long long first_stripe, char **dev);
 
+/* Batched read side for whole stripes (segjerase_read_func, segment/jerasure.c:1255-1631):
+ * dev[i] are device images laid out as lsec_segment_write writes them (NULL = device
+ * unreadable).  Per stripe: majority vote over the stored magics (:1383-1438); stripes with
+ * chunks outside the quorum are rebuilt (decode) and verified against the quorum magic
+ * (jerase_control_check, :202-269), falling back to the brute-force search over erasure
+ * combinations of 1..m devices (jerase_brute_recovery, :321-339); with `paranoid` every
+ * stripe is verified.  Checks and rebuilds run as GPU batches.  User data (nstripes*k*C)
+ * goes to data_out; status[s] (optional) = 0 ok, 1 recovered, 2 blank (zero-filled),
+ * -1 unrecoverable.  Returns the number of unrecoverable stripes, or -1 on error. */
+int lsec_segment_read(lio_erasure_plan_t *plan, char **dev, int nstripes, int chunk, int n_shift,
+                      long long first_stripe, int paranoid, char *data_out, int *status);
+
 /* Pre-build (and cache on the current device) the decode matrix for one erasure pattern,
  * so the first lsec_decode_dev of that pattern does no host work.  0 / -1. */
 int lsec_prepare_decode(lio_erasure_plan_t *plan, const int *erasures);

@@ -71,7 +71,7 @@ class ShardRef(C.Structure):
 EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan", "et_destroy_plan",
            "et_encode", "et_decode", "et_encode_stripes", "et_decode_stripes", "lsec_encode_dev",
            "lsec_decode_dev", "et_encode_stripes_magic", "et_stripes_magic", "lsec_encode_magic_dev",
-           "lsec_stripe_magic_dev", "lsec_segment_write", "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count",
+           "lsec_stripe_magic_dev", "lsec_segment_write", "lsec_segment_read", "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count",
            "lsec_last_error", "lsec_plan_kernel", "lsec_set_kernel_variant")
 
 _lib = None
@@ -120,6 +120,8 @@ def lib():
     L.lsec_encode_magic_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.c_void_p, C.c_void_p]
     L.lsec_stripe_magic_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.c_void_p, C.c_void_p]
     L.lsec_segment_write.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_void_p]
+    L.lsec_segment_read.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_int, C.c_void_p,
+                                    C.c_void_p]
     L.lsec_last_error.restype = C.c_char_p
     L.lsec_plan_kernel.argtypes = [P]
     L.lsec_set_kernel_variant.argtypes = [C.c_int, C.c_int]
@@ -326,6 +328,19 @@ class Plan:
         _check(lib().lsec_segment_write(self._p, data.ctypes.data, n_str, size, n_shift, first_stripe, ptrs),
                "lsec_segment_write")
         return dev
+
+    def segment_read(self, dev: np.ndarray, nstripes: int, chunk: int, n_shift: int = 1, first_stripe: int = 0,
+                     paranoid: bool = False, missing=()):
+        """device images uint8 [k+m, N*(C+4)] -> (data uint8 [N, k, C], status int32 [N], n_unrecoverable)."""
+        n = self.k + self.m
+        addrs = [0 if i in missing else dev[i].ctypes.data for i in range(n)]
+        data = np.zeros((nstripes, self.k, chunk), dtype=np.uint8)
+        status = np.zeros(nstripes, dtype=np.int32)
+        bad = lib().lsec_segment_read(self._p, self._ptr_array(addrs), nstripes, chunk, n_shift, first_stripe,
+                                      int(paranoid), data.ctypes.data, status.ctypes.data)
+        if bad < 0:
+            raise ErasureError(f"lsec_segment_read failed: {last_error()}")
+        return data, status, bad
 
     # -- device-resident calls
     @staticmethod

@@ -58,3 +58,46 @@ def test_segment_write_matches_reference(cuda, method, k, m, chunk, n_shift, fir
         rp = O.RefPlan(method, k, m, 8, p.packet_size)
         ref = rp.segment_write(data, n_str, chunk, n_shift, first)
         assert np.array_equal(ours, ref)
+
+
+@pytest.mark.gpu
+def test_segment_read_quorum_repair_and_brute_force(cuda):
+    k, m, C, N, shift = 6, 3, 16384, 16, 1
+    data = np.stack([stripe(k, C, s) for s in range(N)])
+    lc = C + 4
+    with L.Plan.for_chunk(L.CAUCHY_GOOD, k, m, C) as p:
+        img = p.segment_write(data, shift, 0)
+        out, status, bad = p.segment_read(img, N, C, shift, 0)
+        assert bad == 0 and (status == 0).all() and np.array_equal(out, data)
+
+        def phys(s, j):
+            return (j - s * shift) % (k + m)
+
+        dmg = img.copy()
+        # s0: silent data corruption in data chunk 2 (magic intact) -> only paranoid finds it (brute force)
+        dmg[phys(0, 2), 0 * lc + 4 + 100] ^= 0x5A
+        # s1: bad magic on data chunk 4 -> quorum marks it, rebuild + verify
+        dmg[phys(1, 4), 1 * lc] ^= 1
+        # s2: bad magic on a parity chunk -> data quorum intact, returned as is
+        dmg[phys(2, k + 1), 2 * lc + 1] ^= 1
+        # s3: silent corruption of two chunks -> brute force over pairs
+        dmg[phys(3, 0), 3 * lc + 4 + 7] ^= 0xFF
+        dmg[phys(3, k), 3 * lc + 4 + 9] ^= 0xFF
+        # s4: blank stripe (all magics zero, all data zero)
+        dmg[:, 4 * lc: 5 * lc] = 0
+        # s5: four bad magics -> unrecoverable (count < k)
+        for j in range(4):
+            dmg[phys(5, j), 5 * lc + 2] ^= (j + 1)
+        out, status, bad = p.segment_read(dmg, N, C, shift, 0, paranoid=True)
+        assert status[0] == 1 and status[1] == 1 and status[2] == 0 and status[3] == 1
+        assert status[4] == 2 and status[5] == -1 and bad == 1
+        keep = [s for s in range(N) if s not in (4, 5)]
+        assert np.array_equal(out[keep], data[keep])
+        assert not out[4].any()
+        # without paranoid mode the silently corrupted stripes pass through unchecked (reference behaviour)
+        out, status, bad = p.segment_read(dmg, N, C, shift, 0, paranoid=False)
+        assert status[0] == 0 and not np.array_equal(out[0], data[0])
+        assert status[1] == 1 and np.array_equal(out[1], data[1])
+        # an unreadable device: every stripe rebuilds through decode
+        out, status, bad = p.segment_read(img, N, C, shift, 0, missing=(3,))
+        assert bad == 0 and np.array_equal(out, data)
