@@ -60,11 +60,13 @@ int fail(const char *fmt, ...) {
     if (e_ != hipSuccess) return fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
   } while (0)
 
-enum KernelKind { KNONE = 0, KBYTEWISE = 1, KBITSLICED = 2 };
+enum KernelKind { KNONE = 0, KBYTEWISE = 1, KBITSLICED = 2, KBITMATRIX = 3 };
 
 struct DecodeEntry {
   lsec::gf8::DecodePlan dp;
   std::map<int, CoefCell *> dev_cells;  // device -> e x k cells
+  std::vector<uint32_t> masks;          // bitmatrix codes: (e*w) x k row masks
+  std::map<int, uint32_t *> dev_masks;
 };
 
 struct PlanImpl {
@@ -72,6 +74,8 @@ struct PlanImpl {
   lsec::gf8::Mat coding;   // GF(2^8) matrix the kernels apply (m x k)
   bool coding_ready = false;
   std::map<int, CoefCell *> enc_cells;                   // device -> m x k cells
+  std::vector<uint32_t> enc_masks;                       // bitmatrix codes: (m*w) x k row masks
+  std::map<int, uint32_t *> enc_dev_masks;
   std::map<std::vector<int>, DecodeEntry> decode_cache;  // sorted erased ids -> entry
 };
 
@@ -91,6 +95,8 @@ PlanExt *ext_of(lio_erasure_plan_t *p) {
 }
 
 int kernel_kind(int method, int w) {
+  if (method == BLAUM_ROTH || method == LIBERATION || method == LIBER8TION)
+    return lsec::bitmatrix_w_supported(w) ? KBITMATRIX : KNONE;
   if (w != 8) return KNONE;
   switch (method) {
     case REED_SOL_VAN:
@@ -101,7 +107,7 @@ int kernel_kind(int method, int w) {
     case CAUCHY_GOOD:
       return KBITSLICED;
     default:
-      return KNONE;  // liberation family: bitmatrix-only codes (not GF-linear per byte)
+      return KNONE;
   }
 }
 
@@ -181,6 +187,16 @@ int form_matrices(lio_erasure_plan_t *p, bool with_schedule) {
         std::vector<int> bm(p->encode_bitmatrix, p->encode_bitmatrix + static_cast<size_t>(k) * m * w * w);
         p->encode_schedule = schedule_array(lsec::gf8::smart_schedule(k, m, w, bm));
       }
+      if (!e->impl->coding_ready) {
+        // row masks for the generic bitmatrix kernel: word [(r*w+l)*k + j], bit x = B[r*w+l][j*w+x]
+        auto &mk = e->impl->enc_masks;
+        mk.assign(static_cast<size_t>(m) * w * k, 0u);
+        for (int row = 0; row < m * w; ++row)
+          for (int j = 0; j < k; ++j)
+            for (int x = 0; x < w; ++x)
+              if (p->encode_bitmatrix[static_cast<size_t>(row) * k * w + j * w + x]) mk[static_cast<size_t>(row) * k + j] |= 1u << x;
+        e->impl->coding_ready = true;
+      }
       break;
     }
     default:
@@ -237,12 +253,40 @@ int upload_cells(const std::vector<CoefCell> &h, CoefCell **out) {
   return 0;
 }
 
-// encode matrix cells on the current device
-int encode_cells(PlanExt *e, CoefCell **out) {
+// output rows of the encode image (m; 2 for r6, 1 for raid4)
+int encode_rows(const PlanExt *e) {
+  if (kernel_kind(e->pub.method, e->pub.w) == KBITMATRIX) return e->pub.parity_strips;
+  return static_cast<int>(e->impl->coding.size()) / e->pub.data_strips;
+}
+
+int upload_masks(const std::vector<uint32_t> &h, uint32_t **out) {
+  uint32_t *d = nullptr;
+  HIP_OK(hipMalloc(&d, sizeof(uint32_t) * h.size()));
+  hipError_t err = hipMemcpy(d, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice);
+  if (err != hipSuccess) {
+    (void)hipFree(d);
+    return fail("hipMemcpy(masks): %s", hipGetErrorString(err));
+  }
+  *out = d;
+  return 0;
+}
+
+// encode image on the current device: CoefCell[m][k] (matrix codes) or row masks (bitmatrix)
+int encode_cells(PlanExt *e, const void **out) {
   if (ensure_coding(e)) return -1;
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(e->impl->mu);
+  if (kernel_kind(e->pub.method, e->pub.w) == KBITMATRIX) {
+    auto it = e->impl->enc_dev_masks.find(dev);
+    if (it == e->impl->enc_dev_masks.end()) {
+      uint32_t *d = nullptr;
+      if (upload_masks(e->impl->enc_masks, &d)) return -1;
+      it = e->impl->enc_dev_masks.emplace(dev, d).first;
+    }
+    *out = it->second;
+    return 0;
+  }
   auto it = e->impl->enc_cells.find(dev);
   if (it != e->impl->enc_cells.end()) {
     *out = it->second;
@@ -281,20 +325,39 @@ int parse_erasures(const lio_erasure_plan_t *p, const int *erasures, std::vector
 }
 
 // decode entry (host plan + device cells on the current device)
-int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, CoefCell **cells) {
+int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, const void **cells) {
   if (ensure_coding(e)) return -1;
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(e->impl->mu);
+  const bool bitm = kernel_kind(e->pub.method, e->pub.w) == KBITMATRIX;
   auto it = e->impl->decode_cache.find(ids);
   if (it == e->impl->decode_cache.end()) {
     DecodeEntry ent;
     const int k = e->pub.data_strips;
-    const int m = static_cast<int>(e->impl->coding.size()) / k;
-    if (!lsec::gf8::make_decode(k, m, e->impl->coding, ids, ent.dp)) return fail("decoding matrix is singular");
+    if (bitm) {
+      const lio_erasure_plan_t *p = &e->pub;
+      std::vector<int> bm(p->encode_bitmatrix, p->encode_bitmatrix + static_cast<size_t>(k) * p->parity_strips * p->w * p->w);
+      if (!lsec::gf8::make_bit_decode(k, p->parity_strips, p->w, bm, ids, ent.dp, ent.masks))
+        return fail("decoding bitmatrix is singular");
+    } else {
+      const int m = static_cast<int>(e->impl->coding.size()) / k;
+      if (!lsec::gf8::make_decode(k, m, e->impl->coding, ids, ent.dp)) return fail("decoding matrix is singular");
+    }
     it = e->impl->decode_cache.emplace(ids, std::move(ent)).first;
   }
   DecodeEntry &ent = it->second;
+  if (bitm) {
+    auto dm = ent.dev_masks.find(dev);
+    if (dm == ent.dev_masks.end()) {
+      uint32_t *d = nullptr;
+      if (upload_masks(ent.masks, &d)) return -1;
+      dm = ent.dev_masks.emplace(dev, d).first;
+    }
+    *out = &ent;
+    *cells = dm->second;
+    return 0;
+  }
   auto dc = ent.dev_cells.find(dev);
   if (dc == ent.dev_cells.end()) {
     std::vector<CoefCell> h;
@@ -316,23 +379,32 @@ int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
   const int kind = kernel_kind(p->method, p->w);
   if (kind == KNONE)
     return fail("method %s (w=%d) has no GPU kernel in this build", JE_method[p->method], p->w);
-  if (kind == KBITSLICED) {
-    const long long sp = 8LL * p->packet_size;
+  if (kind == KBITSLICED || kind == KBITMATRIX) {
+    const long long sp = static_cast<long long>(p->w) * p->packet_size;
     if (p->packet_size <= 0 || p->packet_size % 4 != 0 || block_size % sp != 0)
       return fail("block_size %lld is not a multiple of w*packet_size = %lld", block_size, sp);
   }
+  if (kind == KBITMATRIX && m != 2) return fail("%s needs m == 2", JE_method[p->method]);
   return 0;
 }
 
-// Enqueue out[r] = rows[r] . in  for every stripe, splitting R into launches of <= 8 rows.
-int enqueue_apply(int kind, const CoefCell *cells, int K, int R, const ShardRef *in, const ShardRef *out,
-                  int nstripes, long long size, int packet, hipStream_t st) {
-  for (int r0 = 0; r0 < R; r0 += 8) {
+// Enqueue out[r] = rows[r] . in  for every stripe, splitting R into launches of <= 8 rows
+// (<= 2 for the bitmatrix kernel).  `image` is the CoefCell[R][K] matrix image, or for
+// KBITMATRIX the uint32 row masks [(r*w+l)*K + j].
+int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in, const ShardRef *out,
+                  int nstripes, long long size, int packet, hipStream_t st, int w = 8) {
+  const int rmax = kind == KBITMATRIX ? 2 : 8;
+  for (int r0 = 0; r0 < R; r0 += rmax) {
     lsec::ApplyArgs a;
     std::memset(&a, 0, sizeof(a));
     a.K = K;
-    a.R = std::min(8, R - r0);
-    a.cells = cells + static_cast<size_t>(r0) * K;
+    a.R = std::min(rmax, R - r0);
+    if (kind == KBITMATRIX) {
+      a.masks = static_cast<const uint32_t *>(image) + static_cast<size_t>(r0) * w * K;
+      a.w = w;
+    } else {
+      a.cells = static_cast<const CoefCell *>(image) + static_cast<size_t>(r0) * K;
+    }
     a.nstripes = nstripes;
     a.size = size;
     a.packet = packet;
@@ -345,7 +417,9 @@ int enqueue_apply(int kind, const CoefCell *cells, int K, int R, const ShardRef 
       b.nstripes = static_cast<int>(std::min<long long>(per, nstripes - s0));
       for (int j = 0; j < K; ++j) b.in[j].base = in[j].base + static_cast<uint64_t>(s0) * in[j].stride;
       for (int r = 0; r < b.R; ++r) b.out[r].base = out[r0 + r].base + static_cast<uint64_t>(s0) * out[r0 + r].stride;
-      const hipError_t err = kind == KBYTEWISE ? lsec::launch_bytewise(b, st) : lsec::launch_bitsliced(b, st);
+      const hipError_t err = kind == KBYTEWISE    ? lsec::launch_bytewise(b, st)
+                             : kind == KBITMATRIX ? lsec::launch_bitmatrix(b, st)
+                                                  : lsec::launch_bitsliced(b, st);
       if (err != hipSuccess) return fail("kernel launch failed: %s", hipGetErrorString(err));
     }
   }
@@ -357,15 +431,15 @@ int encode_dev(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C, hi
   lio_erasure_plan_t *p = &e->pub;
   if (check_geometry(p, C)) return -1;
   if (nstripes <= 0 || C == 0) return 0;
-  CoefCell *cells = nullptr;
+  const void *cells = nullptr;
   if (encode_cells(e, &cells)) return -1;
   const int k = p->data_strips;
-  const int R = static_cast<int>(e->impl->coding.size()) / k;  // m (2 for r6, 1 for raid4)
+  const int R = encode_rows(e);  // m (2 for r6, 1 for raid4)
   ShardRef in[lsec::kMaxK], out[64];
   if (R > 64) return fail("m=%d too large", R);
   for (int j = 0; j < k; ++j) in[j] = {reinterpret_cast<uint64_t>(sh[j].base), sh[j].stride};
   for (int r = 0; r < R; ++r) out[r] = {reinterpret_cast<uint64_t>(sh[k + r].base), sh[k + r].stride};
-  return enqueue_apply(kernel_kind(p->method, p->w), cells, k, R, in, out, nstripes, C, p->packet_size, st);
+  return enqueue_apply(kernel_kind(p->method, p->w), cells, k, R, in, out, nstripes, C, p->packet_size, st, p->w);
 }
 
 // returns 0 (done or nothing to do) / -1
@@ -380,7 +454,7 @@ int decode_dev(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C, co
   if (p->method == RAID4 && ids[0] >= p->data_strips) return 0;  // raid4.c:48 leaves lost parity alone
   if (nstripes <= 0 || C == 0) return 0;
   DecodeEntry *ent = nullptr;
-  CoefCell *cells = nullptr;
+  const void *cells = nullptr;
   if (decode_entry(e, ids, &ent, &cells)) return -1;
   const int k = p->data_strips;
   ShardRef in[lsec::kMaxK], out[64];
@@ -393,7 +467,7 @@ int decode_dev(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C, co
     const lsec_shard_t &s = sh[ent->dp.erased[r]];
     out[r] = {reinterpret_cast<uint64_t>(s.base), s.stride};
   }
-  return enqueue_apply(kernel_kind(p->method, p->w), cells, k, R, in, out, nstripes, C, p->packet_size, st);
+  return enqueue_apply(kernel_kind(p->method, p->w), cells, k, R, in, out, nstripes, C, p->packet_size, st, p->w);
 }
 
 // ---------------------------------------------------------------- host copy pool
@@ -590,7 +664,7 @@ size_t staging_budget() {
 // bytewise on any 8-byte boundary, bitsliced on super-packet boundaries -- so a block is a
 // valid independent sub-stripe).
 int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
-             const std::vector<int> &out_ids, const CoefCell *cells, int kind, uint8_t *magic_host = nullptr) {
+             const std::vector<int> &out_ids, const void *cells, int kind, uint8_t *magic_host = nullptr) {
   lio_erasure_plan_t *p = &e->pub;
   const int km = p->data_strips + p->parity_strips;
   // staged position of every device id (for the stripe magic, which covers all k+m chunks)
@@ -673,7 +747,7 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
         in[j] = {reinterpret_cast<uint64_t>(sl.d) + static_cast<uint64_t>(j) * len, static_cast<int64_t>(nin * len)};
       for (int r = 0; r < nout; ++r)
         out[r] = {reinterpret_cast<uint64_t>(sl.d) + out_off + static_cast<uint64_t>(r) * len, static_cast<int64_t>(nout * len)};
-      if (nout > 0 && (rc = enqueue_apply(kind, cells, nin, nout, in, out, nb, clen, p->packet_size, stg->s_out))) break;
+      if (nout > 0 && (rc = enqueue_apply(kind, cells, nin, nout, in, out, nb, clen, p->packet_size, stg->s_out, p->w))) break;
       if (magic_host) {
         lsec::MagicArgs ma;
         std::memset(&ma, 0, sizeof(ma));
@@ -774,10 +848,10 @@ int encode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C) {
     HIP_OK(hipStreamSynchronize(st));
     return 0;
   }
-  CoefCell *cells = nullptr;
+  const void *cells = nullptr;
   if (encode_cells(e, &cells)) return -1;
   const int k = p->data_strips;
-  const int R = static_cast<int>(e->impl->coding.size()) / k;
+  const int R = encode_rows(e);
   std::vector<int> in_ids(k), out_ids(R);
   for (int j = 0; j < k; ++j) in_ids[j] = j;
   for (int r = 0; r < R; ++r) out_ids[r] = k + r;
@@ -803,7 +877,7 @@ int decode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C, cons
     return 0;
   }
   DecodeEntry *ent = nullptr;
-  CoefCell *cells = nullptr;
+  const void *cells = nullptr;
   if (decode_entry(e, ids, &ent, &cells)) return -1;
   return run_host(e, ptrs, nstripes, C, ent->dp.survivors, ent->dp.erased, cells, kernel_kind(p->method, p->w));
 }
@@ -813,10 +887,10 @@ int encode_stripes_magic_impl(PlanExt *e, char **ptrs, int nstripes, long long C
   if (!ptrs || !magic) return fail("ptrs / magic is NULL");
   if (check_geometry(p, C)) return -1;
   if (nstripes <= 0 || C == 0) return 0;
-  CoefCell *cells = nullptr;
+  const void *cells = nullptr;
   if (encode_cells(e, &cells)) return -1;
   const int k = p->data_strips;
-  const int R = static_cast<int>(e->impl->coding.size()) / k;
+  const int R = encode_rows(e);
   if (R != p->parity_strips) return fail("stripe magic needs m parity rows");
   std::vector<int> in_ids(k), out_ids(R);
   for (int j = 0; j < k; ++j) in_ids[j] = j;
@@ -992,11 +1066,20 @@ void et_destroy_plan(lio_erasure_plan_t *p) {
       (void)hipSetDevice(kv.first);
       (void)hipFree(kv.second);
     }
-    for (auto &ent : e->impl->decode_cache)
+    for (auto &kv : e->impl->enc_dev_masks) {
+      (void)hipSetDevice(kv.first);
+      (void)hipFree(kv.second);
+    }
+    for (auto &ent : e->impl->decode_cache) {
       for (auto &kv : ent.second.dev_cells) {
         (void)hipSetDevice(kv.first);
         (void)hipFree(kv.second);
       }
+      for (auto &kv : ent.second.dev_masks) {
+        (void)hipSetDevice(kv.first);
+        (void)hipFree(kv.second);
+      }
+    }
     if (cur >= 0) (void)hipSetDevice(cur);
     delete e->impl;
     e->magic = 0;
@@ -1249,7 +1332,7 @@ int lsec_prepare_decode(lio_erasure_plan_t *plan, const int *erasures) {
   const int pr = parse_erasures(plan, erasures, ids);
   if (pr != 0) return pr < 0 ? -1 : 0;
   DecodeEntry *ent = nullptr;
-  CoefCell *cells = nullptr;
+  const void *cells = nullptr;
   return decode_entry(e, ids, &ent, &cells);
 }
 

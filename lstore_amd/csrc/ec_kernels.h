@@ -46,8 +46,10 @@ struct ApplyArgs {
   const CoefCell *cells;  // R x K, row-major (device memory)
   int K, R;
   int nstripes;
-  int packet;             // bitsliced only: packet size P (bytes)
+  int packet;             // bitsliced / bitmatrix: packet size P (bytes)
   int64_t size;           // bytes per shard (chunk C)
+  const uint32_t *masks;  // bitmatrix only: (R*w) x K words, bit x of [(r*w+l)*K + j] = B[r*w+l][j*w+x]
+  int w;                  // bitmatrix only: packets per super-packet
   ShardRef in[kMaxK];
   ShardRef out[kMaxR];
 };
@@ -83,6 +85,10 @@ void make_cell(uint8_t c, CoefCell &cell);
 // Launchers (return hipError_t of the launch).  grid_blocks <= 0 picks a default.
 hipError_t launch_bytewise(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
 hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
+// generic GF(2) bitmatrix codes (liberation / blaum_roth / liber8tion, liberation.c): any w in
+// kBitmatrixW, R <= 2 (these codes have m = 2)
+hipError_t launch_bitmatrix(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
+bool bitmatrix_w_supported(int w);
 
 // Variant selection knobs for experiments: 0 = default
 void set_kernel_variant(int bytewise_variant, int bitsliced_variant);

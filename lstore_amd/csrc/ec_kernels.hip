@@ -78,6 +78,29 @@ hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid_blocks)
   return by_r(a.R, [&](auto r) { return dispatch_bitsliced<decltype(r)::value>(a, st, grid, dw); });
 }
 
+bool bitmatrix_w_supported(int w) {
+  switch (w) {
+#define LSEC_BM_CASE(WW) case WW:
+    LSEC_BITMATRIX_W(LSEC_BM_CASE)
+#undef LSEC_BM_CASE
+    return true;
+    default:
+      return false;
+  }
+}
+
+hipError_t launch_bitmatrix(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
+  if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > 2 || !bitmatrix_w_supported(a.w) || !a.masks ||
+      a.packet <= 0 || a.packet % 4 != 0 || a.size % (static_cast<int64_t>(a.w) * a.packet) != 0)
+    return hipErrorInvalidValue;
+  if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
+  const uint64_t col_bytes = a.size / a.w;
+  const uint64_t ntiles = ((col_bytes + kBlock * 4 - 1) / (kBlock * 4)) * static_cast<uint64_t>(a.nstripes);
+  if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
+  const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);
+  return by_r(a.R, [&](auto r) { return dispatch_bitmatrix<decltype(r)::value>(a, st, grid); });
+}
+
 // ------------------------------------------------------------------ stripe magic (adler32)
 namespace {
 

@@ -285,6 +285,65 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ generic bitmatrix
+// Bitmatrix codes that are not GF(2^8)-linear per byte (liberation / blaum_roth / liber8tion,
+// vendor/jerasure/src/liberation.c): packet l of output r = XOR of the input packets (j, x)
+// whose bit B[r*w+l][j*w+x] is set (jerasure_bitmatrix_dotprod, jerasure.c:317-362).  A lane
+// owns one dword column of a super-packet and applies the bitmatrix under wave-uniform
+// branches (the row masks live in the constant address space).
+typedef const __attribute__((address_space(4))) uint32_t ConstU32;
+
+template <int R, int W>
+__global__ __launch_bounds__(kBlock) void k_bitmatrix(ApplyArgs a) {
+  const int K = a.K;
+  const uint32_t P = static_cast<uint32_t>(a.packet);
+  const uint32_t col_bytes = static_cast<uint32_t>(a.size / W);  // nsuper * P
+  constexpr uint32_t kTile = kBlock * 4;
+  const uint32_t tiles_per_stripe = (col_bytes + kTile - 1) / kTile;
+  const uint32_t ntiles = tiles_per_stripe * static_cast<uint32_t>(a.nstripes);
+  ConstU32 *masks = reinterpret_cast<ConstU32 *>(reinterpret_cast<uintptr_t>(a.masks));
+  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+    const uint32_t s = t / tiles_per_stripe;
+    const uint32_t colb = (t - s * tiles_per_stripe) * kTile + threadIdx.x * 4;
+    if (colb >= col_bytes) continue;
+    const uint32_t sp = colb / P;
+    const int64_t off = static_cast<int64_t>(sp) * W * P + (colb - sp * P);
+    uint32_t acc[R][W];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int l = 0; l < W; ++l) acc[r][l] = 0u;
+    for (int j = 0; j < K; ++j) {
+      const uint64_t p = a.in[j].base + s * a.in[j].stride + off;
+      uint32_t e[W];
+#pragma unroll
+      for (int x = 0; x < W; ++x) e[x] = __builtin_nontemporal_load(gptr<uint32_t>(p + x * P));
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int l = 0; l < W; ++l) {
+          const uint32_t mask = masks[(r * W + l) * K + j];
+          uint32_t v = 0;
+#pragma unroll
+          for (int x = 0; x < W; ++x)
+            if ((mask >> x) & 1u) v ^= e[x];
+          acc[r][l] ^= v;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
+#pragma unroll
+      for (int l = 0; l < W; ++l) __builtin_nontemporal_store(acc[r][l], gptr_w<uint32_t>(q + l * P));
+    }
+  }
+}
+
+// word sizes the liberation family can produce: primes (liberation), p-1 for prime p
+// (blaum_roth), 8 (liber8tion)
+#define LSEC_BITMATRIX_W(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(10) X(11) X(12) X(13) X(16) X(17) \
+                            X(18) X(19) X(22) X(23) X(28) X(29) X(30) X(31)
+
 // ------------------------------------------------------------------ per-R dispatch
 template <int R, int IT, int MINW>
 hipError_t bytewise_k(const ApplyArgs &a, hipStream_t st, int grid) {
@@ -320,9 +379,26 @@ hipError_t dispatch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid, int 
   return hipGetLastError();
 }
 
+template <int R>
+hipError_t dispatch_bitmatrix(const ApplyArgs &a, hipStream_t st, int grid) {
+  if constexpr (R <= 2) {
+    switch (a.w) {
+#define LSEC_BM_W(WW) \
+  case WW: hipLaunchKernelGGL((k_bitmatrix<R, WW>), dim3(grid), dim3(kBlock), 0, st, a); break;
+      LSEC_BITMATRIX_W(LSEC_BM_W)
+#undef LSEC_BM_W
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  } else {
+    return hipErrorInvalidValue;
+  }
+}
+
 #define LSEC_DECLARE_R(RR)                                                                         \
   extern template hipError_t dispatch_bytewise<RR>(const ApplyArgs &, hipStream_t, int, int);      \
-  extern template hipError_t dispatch_bitsliced<RR>(const ApplyArgs &, hipStream_t, int, int);
+  extern template hipError_t dispatch_bitsliced<RR>(const ApplyArgs &, hipStream_t, int, int);         \
+  extern template hipError_t dispatch_bitmatrix<RR>(const ApplyArgs &, hipStream_t, int);
 #ifndef LSEC_INSTANTIATING
 LSEC_DECLARE_R(1) LSEC_DECLARE_R(2) LSEC_DECLARE_R(3) LSEC_DECLARE_R(4)
 LSEC_DECLARE_R(5) LSEC_DECLARE_R(6) LSEC_DECLARE_R(7) LSEC_DECLARE_R(8)

@@ -289,6 +289,71 @@ bool make_decode(int k, int m, const Mat &coding, const std::vector<int> &erased
   return true;
 }
 
+bool make_bit_decode(int k, int m, int w, const std::vector<int> &bm, const std::vector<int> &erased_ids,
+                     DecodePlan &dp, std::vector<uint32_t> &masks) {
+  std::vector<char> lost(k + m, 0);
+  for (int e : erased_ids) {
+    if (e < 0 || e >= k + m) return false;
+    lost[e] = 1;
+  }
+  dp.erased.clear();
+  dp.survivors.clear();
+  for (int i = 0; i < k + m; ++i) {
+    if (lost[i]) dp.erased.push_back(i);
+    else if (static_cast<int>(dp.survivors.size()) < k) dp.survivors.push_back(i);
+  }
+  if (static_cast<int>(dp.survivors.size()) < k) return false;
+  const int n = k * w;
+  // S: survivor bit-rows in terms of the data bits; rows packed as bitsets of n bits
+  const int words = (n + 63) / 64;
+  auto bit = [&](std::vector<uint64_t> &row, int c) { row[c / 64] |= 1ull << (c % 64); };
+  std::vector<std::vector<uint64_t>> a(n, std::vector<uint64_t>(words, 0)), inv(n, std::vector<uint64_t>(words, 0));
+  for (int j = 0; j < k; ++j) {
+    const int id = dp.survivors[j];
+    for (int l = 0; l < w; ++l) {
+      auto &row = a[j * w + l];
+      if (id < k) {
+        bit(row, id * w + l);
+      } else {
+        const int *src = &bm[static_cast<size_t>((id - k) * w + l) * n];
+        for (int c = 0; c < n; ++c)
+          if (src[c]) bit(row, c);
+      }
+    }
+  }
+  for (int i = 0; i < n; ++i) bit(inv[i], i);
+  for (int c = 0; c < n; ++c) {  // Gauss-Jordan over GF(2)
+    int p = c;
+    while (p < n && !((a[p][c / 64] >> (c % 64)) & 1)) ++p;
+    if (p == n) return false;
+    std::swap(a[p], a[c]);
+    std::swap(inv[p], inv[c]);
+    for (int r = 0; r < n; ++r)
+      if (r != c && ((a[r][c / 64] >> (c % 64)) & 1))
+        for (int x = 0; x < words; ++x) { a[r][x] ^= a[c][x]; inv[r][x] ^= inv[c][x]; }
+  }
+  // output bit-rows: erased data i -> inv rows i*w..; erased coding c -> B_c x inv
+  const int e = static_cast<int>(dp.erased.size());
+  masks.assign(static_cast<size_t>(e) * w * k, 0u);
+  for (int r = 0; r < e; ++r) {
+    const int id = dp.erased[r];
+    for (int l = 0; l < w; ++l) {
+      std::vector<uint64_t> row(words, 0);
+      if (id < k) {
+        row = inv[id * w + l];
+      } else {
+        const int *src = &bm[static_cast<size_t>((id - k) * w + l) * n];
+        for (int c = 0; c < n; ++c)
+          if (src[c])
+            for (int x = 0; x < words; ++x) row[x] ^= inv[c][x];
+      }
+      for (int c = 0; c < n; ++c)
+        if ((row[c / 64] >> (c % 64)) & 1) masks[static_cast<size_t>(r * w + l) * k + c / w] |= 1u << (c % w);
+    }
+  }
+  return true;
+}
+
 // ---------------------------------------------------------------- liberation family
 // Layout helper: a (2w) x (kw) bitmatrix whose first w rows are [I I ... I].
 static std::vector<int> identity_top(int k, int w) {

@@ -15,7 +15,8 @@ from patterns import affine, stripe
 
 pytestmark = pytest.mark.gpu
 
-GPU_METHODS = (L.REED_SOL_VAN, L.REED_SOL_R6_OP, L.CAUCHY_ORIG, L.CAUCHY_GOOD, L.RAID4)
+GPU_METHODS = (L.REED_SOL_VAN, L.REED_SOL_R6_OP, L.CAUCHY_ORIG, L.CAUCHY_GOOD, L.RAID4, L.LIBERATION, L.BLAUM_ROTH,
+               L.LIBER8TION)
 
 
 def case_input(v):
@@ -50,6 +51,30 @@ def test_encode_block_matches_reference(cuda, golden):
             assert np.array_equal(par, golden["small"][v["full"]])
         n += 1
     assert n >= 30
+
+
+@pytest.mark.parametrize("method,k,w", [(L.LIBERATION, 7, 7), (L.LIBERATION, 11, 11), (L.BLAUM_ROTH, 10, 10),
+                                        (L.BLAUM_ROTH, 4, 4), (L.LIBER8TION, 8, 8), (L.LIBER8TION, 3, 8)])
+def test_liberation_family_vs_reference(cuda, method, k, w):
+    """Generic GF(2) bitmatrix kernel vs the real reference (oracle/_ref) for every family member."""
+    if not O.ref_available():
+        pytest.skip("oracle/_ref not built")
+    m, P = 2, 32
+    size = w * P * 5
+    data = stripe(k, size, w)
+    rp = O.RefPlan(method, k, m, w, P)
+    ref = rp.encode(data)
+    par = np.zeros((m, size), np.uint8)
+    with L.Plan.new(method, size, k, m, w, P, 8) as p:
+        p.form_encoding_matrix()
+        p.encode_block([data[j] for j in range(k)] + [par[i] for i in range(m)])
+        assert np.array_equal(par, ref)
+        full = np.vstack([data, par])
+        for er in ([0], [k - 1], [k], [k + 1], [0, k - 1], [1, k], [k, k + 1]):
+            sh = full.copy()
+            sh[er] = 0
+            assert p.decode_block([sh[i] for i in range(k + m)], er) == 0
+            assert np.array_equal(sh, full), er
 
 
 # ---------------------------------------------------------------- encode, device-resident

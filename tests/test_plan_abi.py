@@ -173,8 +173,10 @@ def test_no_gpu_means_loud_failure(built):
 
 
 def test_unsupported_method_is_an_error_not_a_fallback(built):
-    with L.Plan.generate(6 * 7 * 64 * 4, L.LIBERATION, 6, 2) as p:
+    with L.Plan.new(L.REED_SOL_VAN, 0, 6, 3, 16, 8, 8) as p:   # w = 16: no GPU kernel in this build
         assert p.kernel == 0
-        st = np.zeros((1, 8, p.w * p.packet_size), np.uint8)
+        st = np.zeros((1, 9, 4096), np.uint8)
         with pytest.raises(E.ErasureError, match="no GPU kernel"):
             p.encode_stripes(st)
+    with L.Plan.generate(6 * 7 * 64 * 4, L.LIBERATION, 6, 2) as p:
+        assert p.kernel == 3   # generic bitmatrix kernel
