@@ -36,12 +36,15 @@ hipError_t by_r(int R, F f) {
   }
 }
 
-// (IT, MINW) shape for a K x R bytewise launch.  variant 0 = automatic policy, measured
-// (tools/kbench.py): two 4 KiB steps per lane while all K*IT loads of a lane fit the register
-// file at >= 2 waves/SIMD; the widest shapes (K*R >= 100, e.g. RS(20+6)) drop to one step.
+// Launch shape for a K x R bytewise launch (codes in ec_kernels_impl.h).  variant 0 = the
+// automatic policy measured with tools/kbench.py (profiles/r01_v3_kbench_vw.txt):
+//   R == 1 (single-erasure decode: XOR-heavy, read-bound)  8 B per lane        (+1.5-2 %)
+//   K*R >= 48 (wide encodes: VALU-heavy, register-bound)    2 x 8 B per lane    (+6-9 %)
+//   otherwise                                                2 x 16 B per lane
 int bytewise_shape(int K, int R) {
-  if (g_bw_variant > 0) return g_bw_variant - 1;
-  return K * R >= 100 ? 1 : 0;
+  if (g_bw_variant > 0) return (g_bw_variant - 1) % kBwShapes;
+  if (R == 1) return 3;
+  return K * R >= 48 ? 2 : 0;
 }
 
 }  // namespace
@@ -55,8 +58,7 @@ hipError_t launch_bytewise(const ApplyArgs &a, hipStream_t st, int grid_blocks) 
   if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > 8 || a.size % 8 != 0) return hipErrorInvalidValue;
   if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
   const int shape = bytewise_shape(a.K, a.R);
-  const int it = (shape == 1 || shape == 3) ? 1 : 2;
-  const uint64_t tile = static_cast<uint64_t>(kBlock) * 16 * it;
+  const uint64_t tile = static_cast<uint64_t>(kBlock) * 4 * bw_shape_vw(shape) * bw_shape_it(shape);
   const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);

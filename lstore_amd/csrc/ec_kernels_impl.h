@@ -76,13 +76,6 @@ __device__ __forceinline__ uint32_t gf_mul_acc(uint32_t acc, uint32_t ia, uint32
          __builtin_amdgcn_perm(t[5], t[4], ic);
 }
 
-// Per-lane work unit of the bytewise kernel: 16 bytes (one dwordx4) per step, IT steps
-// 4 KiB apart per tile (tile = 256 * 16 * IT bytes of every shard).
-template <int IT>
-struct BwTile {
-  static constexpr int kBytes = kBlock * 16 * IT;
-};
-
 // Spread the grid so that each XCD (blocks b, b+8, b+16, ... are dealt to one XCD) gets a
 // contiguous run of tiles instead of every 8th tile: measured +2-3% HBM throughput on this
 // streaming pattern (tools/kprobe.hip).  Bijective for any grid size; placement is only a
@@ -92,12 +85,22 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
   return xcd * per + min(xcd, rem) + (b >> 3);
 }
 
-template <int R, int kBwIt>
-__device__ __forceinline__ void bw_accumulate(u32x4 (&acc)[kBwIt][R], const u32x4 (&v)[kBwIt],
-                                              ConstCell *cells, int K, int j) {
-  u32x4 ia[kBwIt], ib[kBwIt], ic[kBwIt];
+// Per-lane work unit of the bytewise kernel: VW dwords (16 B for VW = 4, 8 B for VW = 2) per
+// step, IT steps kBlock*4*VW bytes apart; a tile is kBlock*4*VW*IT bytes of every shard.
+template <int IT, int VW>
+struct BwTile {
+  static constexpr int kStep = kBlock * 4 * VW;
+  static constexpr int kBytes = kStep * IT;
+};
+
+template <int R, int IT, int VW>
+__device__ __forceinline__ void bw_accumulate(typename VecT<VW>::type (&acc)[IT][R],
+                                              const typename VecT<VW>::type (&v)[IT], ConstCell *cells, int K,
+                                              int j) {
+  typedef typename VecT<VW>::type V;
+  V ia[IT], ib[IT], ic[IT];
 #pragma unroll
-  for (int it = 0; it < kBwIt; ++it) {
+  for (int it = 0; it < IT; ++it) {
     ia[it] = v[it] & 0x07070707u;
     ib[it] = (v[it] >> 3) & 0x07070707u;
     ic[it] = (v[it] >> 6) & 0x03030303u;
@@ -109,109 +112,107 @@ __device__ __forceinline__ void bw_accumulate(u32x4 (&acc)[kBwIt][R], const u32x
     if (c == 0) continue;
     if (c == 1) {
 #pragma unroll
-      for (int it = 0; it < kBwIt; ++it) acc[it][r] ^= v[it];
+      for (int it = 0; it < IT; ++it) acc[it][r] ^= v[it];
       continue;
     }
     const uint32_t t[6] = {cell->ta_lo, cell->ta_hi, cell->tb_lo, cell->tb_hi, cell->tc_lo, cell->tc_hi};
 #pragma unroll
-    for (int it = 0; it < kBwIt; ++it)
+    for (int it = 0; it < IT; ++it)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[it][r][e] = gf_mul_acc(acc[it][r][e], ia[it][e], ib[it][e], ic[it][e], t);
+      for (int e = 0; e < VW; ++e) acc[it][r][e] = gf_mul_acc(acc[it][r][e], ia[it][e], ib[it][e], ic[it][e], t);
   }
 }
 
-// MINW = minimum waves per SIMD the register allocation must allow (1 = unconstrained;
-// 4 caps the kernel at 128 VGPRs so wide K*R shapes keep enough waves to hide latency).
-template <int R, int KC, int kBwIt, int MINW>
+// MINW = minimum waves per SIMD the register allocation must allow (1 = unconstrained).
+template <int R, int KC, int IT, int MINW, int VW>
 __global__ __launch_bounds__(kBlock, MINW) void k_gf8_bytewise(ApplyArgs a) {
-  constexpr int kBwTile = BwTile<kBwIt>::kBytes;
+  typedef typename VecT<VW>::type V;
+  constexpr int kStep = BwTile<IT, VW>::kStep;
+  constexpr int kTile = BwTile<IT, VW>::kBytes;
+  constexpr int kLane = 4 * VW;
   const int K = KC ? KC : a.K;
   const int64_t C = a.size;
-  const uint32_t tiles_per_stripe = static_cast<uint32_t>((C + kBwTile - 1) / kBwTile);
+  const uint32_t tiles_per_stripe = static_cast<uint32_t>((C + kTile - 1) / kTile);
   const uint32_t ntiles = tiles_per_stripe * static_cast<uint32_t>(a.nstripes);
   ConstCell *cells = const_cells(a.cells);
 
   for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
     const uint32_t s = t / tiles_per_stripe;
-    const int64_t off0 = static_cast<int64_t>(t - s * tiles_per_stripe) * kBwTile + threadIdx.x * 16;
-    const bool full = (static_cast<int64_t>(t - s * tiles_per_stripe) + 1) * kBwTile <= C;  // wave-uniform
+    const int64_t off0 = static_cast<int64_t>(t - s * tiles_per_stripe) * kTile + threadIdx.x * kLane;
+    const bool full = (static_cast<int64_t>(t - s * tiles_per_stripe) + 1) * kTile <= C;  // wave-uniform
 
-    u32x4 acc[kBwIt][R];
+    V acc[IT][R];
 #pragma unroll
-    for (int it = 0; it < kBwIt; ++it)
+    for (int it = 0; it < IT; ++it)
 #pragma unroll
       for (int r = 0; r < R; ++r) acc[it][r] = 0u;
 
     if (full) {
       if constexpr (KC > 0) {
         // all K*IT loads in flight before any arithmetic
-        u32x4 v[KC][kBwIt];
+        V v[KC][IT];
 #pragma unroll
         for (int j = 0; j < KC; ++j) {
           const uint64_t p = a.in[j].base + s * a.in[j].stride + off0;
 #pragma unroll
-          for (int it = 0; it < kBwIt; ++it)
-            v[j][it] = __builtin_nontemporal_load(gptr<u32x4>(p + it * kBlock * 16));
+          for (int it = 0; it < IT; ++it) v[j][it] = __builtin_nontemporal_load(gptr<V>(p + it * kStep));
         }
 #pragma unroll
-        for (int j = 0; j < KC; ++j) bw_accumulate<R, kBwIt>(acc, v[j], cells, K, j);
+        for (int j = 0; j < KC; ++j) bw_accumulate<R, IT, VW>(acc, v[j], cells, K, j);
       } else {
         for (int j0 = 0; j0 < K; j0 += 4) {
-          u32x4 v[4][kBwIt];
+          V v[4][IT];
           const int nj = min(4, K - j0);
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj) {
             if (jj < nj) {
-              const int j = j0 + jj;
-              const uint64_t p = a.in[j].base + s * a.in[j].stride + off0;
+              const uint64_t p = a.in[j0 + jj].base + s * a.in[j0 + jj].stride + off0;
 #pragma unroll
-              for (int it = 0; it < kBwIt; ++it)
-                v[jj][it] = __builtin_nontemporal_load(gptr<u32x4>(p + it * kBlock * 16));
+              for (int it = 0; it < IT; ++it) v[jj][it] = __builtin_nontemporal_load(gptr<V>(p + it * kStep));
             }
           }
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj)
-            if (jj < nj) bw_accumulate<R, kBwIt>(acc, v[jj], cells, K, j0 + jj);
+            if (jj < nj) bw_accumulate<R, IT, VW>(acc, v[jj], cells, K, j0 + jj);
         }
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const uint64_t q = a.out[r].base + s * a.out[r].stride + off0;
 #pragma unroll
-        for (int it = 0; it < kBwIt; ++it)
-          __builtin_nontemporal_store(acc[it][r], gptr_w<u32x4>(q + it * kBlock * 16));
+        for (int it = 0; it < IT; ++it) __builtin_nontemporal_store(acc[it][r], gptr_w<V>(q + it * kStep));
       }
     } else {
-      // ragged last tile: C is a multiple of 8, so each lane handles 16, 8 or 0 bytes per step
+      // ragged last tile: C is a multiple of 8, so a 16-byte lane unit may be half full
       for (int j = 0; j < K; ++j) {
         const uint64_t p = a.in[j].base + s * a.in[j].stride;
-        u32x4 v[kBwIt];
+        V v[IT];
 #pragma unroll
-        for (int it = 0; it < kBwIt; ++it) {
-          const int64_t o = off0 + it * kBlock * 16;
+        for (int it = 0; it < IT; ++it) {
+          const int64_t o = off0 + it * kStep;
           v[it] = 0u;
-          if (o + 16 <= C) {
-            v[it] = *gptr<u32x4>(p + o);
+          if (o + kLane <= C) {
+            v[it] = *gptr<V>(p + o);
           } else if (o < C) {
             const u32x2 h = *gptr<u32x2>(p + o);
-            v[it].x = h.x;
-            v[it].y = h.y;
+            v[it][0] = h.x;
+            v[it][1] = h.y;
           }
         }
-        bw_accumulate<R, kBwIt>(acc, v, cells, K, j);
+        bw_accumulate<R, IT, VW>(acc, v, cells, K, j);
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const uint64_t q = a.out[r].base + s * a.out[r].stride;
 #pragma unroll
-        for (int it = 0; it < kBwIt; ++it) {
-          const int64_t o = off0 + it * kBlock * 16;
-          if (o + 16 <= C) {
-            *gptr_w<u32x4>(q + o) = acc[it][r];
+        for (int it = 0; it < IT; ++it) {
+          const int64_t o = off0 + it * kStep;
+          if (o + kLane <= C) {
+            *gptr_w<V>(q + o) = acc[it][r];
           } else if (o < C) {
             u32x2 h;
-            h.x = acc[it][r].x;
-            h.y = acc[it][r].y;
+            h.x = acc[it][r][0];
+            h.y = acc[it][r][1];
             *gptr_w<u32x2>(q + o) = h;
           }
         }
@@ -345,27 +346,32 @@ __global__ __launch_bounds__(kBlock) void k_bitmatrix(ApplyArgs a) {
                             X(18) X(19) X(22) X(23) X(28) X(29) X(30) X(31)
 
 // ------------------------------------------------------------------ per-R dispatch
-template <int R, int IT, int MINW>
+template <int R, int IT, int MINW, int VW>
 hipError_t bytewise_k(const ApplyArgs &a, hipStream_t st, int grid) {
   switch (a.K) {
 #define LSEC_BW_K(KK) \
-  case KK: hipLaunchKernelGGL((k_gf8_bytewise<R, KK, IT, MINW>), dim3(grid), dim3(kBlock), 0, st, a); break;
+  case KK: hipLaunchKernelGGL((k_gf8_bytewise<R, KK, IT, MINW, VW>), dim3(grid), dim3(kBlock), 0, st, a); break;
     LSEC_BW_K(4) LSEC_BW_K(6) LSEC_BW_K(8) LSEC_BW_K(10) LSEC_BW_K(12) LSEC_BW_K(16) LSEC_BW_K(20)
 #undef LSEC_BW_K
-    default: hipLaunchKernelGGL((k_gf8_bytewise<R, 0, IT, MINW>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    default: hipLaunchKernelGGL((k_gf8_bytewise<R, 0, IT, MINW, VW>), dim3(grid), dim3(kBlock), 0, st, a); break;
   }
   return hipGetLastError();
 }
 
-// shape = (IT, MINW) code: 0 -> (2,1), 1 -> (1,1), 2 -> (2,4), 3 -> (1,4), 4 -> (2,3)
+// Bytewise launch shapes (tile per lane):  code -> (IT, VW)   [all MINW = 1]
+//   0 -> (2, 4) 32 B/lane    1 -> (1, 4) 16 B/lane    2 -> (2, 2) 16 B/lane in 8 B pieces
+//   3 -> (1, 2)  8 B/lane
+constexpr int kBwShapes = 4;
+inline int bw_shape_it(int shape) { return (shape == 0 || shape == 2) ? 2 : 1; }
+inline int bw_shape_vw(int shape) { return shape <= 1 ? 4 : 2; }
+
 template <int R>
 hipError_t dispatch_bytewise(const ApplyArgs &a, hipStream_t st, int grid, int shape) {
   switch (shape) {
-    case 1: return bytewise_k<R, 1, 1>(a, st, grid);
-    case 2: return bytewise_k<R, 2, 4>(a, st, grid);
-    case 3: return bytewise_k<R, 1, 4>(a, st, grid);
-    case 4: return bytewise_k<R, 2, 3>(a, st, grid);
-    default: return bytewise_k<R, 2, 1>(a, st, grid);
+    case 1: return bytewise_k<R, 1, 1, 4>(a, st, grid);
+    case 2: return bytewise_k<R, 2, 1, 2>(a, st, grid);
+    case 3: return bytewise_k<R, 1, 1, 2>(a, st, grid);
+    default: return bytewise_k<R, 2, 1, 4>(a, st, grid);
   }
 }
 
