@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -60,21 +61,23 @@ int fail(const char *fmt, ...) {
     if (e_ != hipSuccess) return fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
   } while (0)
 
-enum KernelKind { KNONE = 0, KBYTEWISE = 1, KBITSLICED = 2, KBITMATRIX = 3 };
+enum KernelKind { KNONE = 0, KBYTEWISE = 1, KBITSLICED = 2, KBITMATRIX = 3, KWORDWISE = 4 };
 
 struct DecodeEntry {
   lsec::gf8::DecodePlan dp;
   std::map<int, CoefCell *> dev_cells;  // device -> e x k cells
-  std::vector<uint32_t> masks;          // bitmatrix codes: (e*w) x k row masks
+  std::vector<uint32_t> masks;          // bitmatrix codes: (e*w) x k row masks; wordwise: e x k x w products
   std::map<int, uint32_t *> dev_masks;
 };
 
 struct PlanImpl {
   std::mutex mu;
   lsec::gf8::Mat coding;   // GF(2^8) matrix the kernels apply (m x k)
+  lsec::gfw::Mat coding_w; // GF(2^16) / GF(2^32) matrix codes (m x k)
   bool coding_ready = false;
   std::map<int, CoefCell *> enc_cells;                   // device -> m x k cells
-  std::vector<uint32_t> enc_masks;                       // bitmatrix codes: (m*w) x k row masks
+  std::vector<uint32_t> enc_masks;                       // bitmatrix codes: (m*w) x k row masks;
+                                                         // wordwise: m x k x w products
   std::map<int, uint32_t *> enc_dev_masks;
   std::map<std::vector<int>, DecodeEntry> decode_cache;  // sorted erased ids -> entry
 };
@@ -94,21 +97,52 @@ PlanExt *ext_of(lio_erasure_plan_t *p) {
   return e->magic == kPlanMagic ? e : nullptr;
 }
 
+bool liberation_family(int method) { return method == BLAUM_ROTH || method == LIBERATION || method == LIBER8TION; }
+
+// Which kernel applies a plan:
+//   RS / r6 at w = 8 -> bytewise GF(2^8); at w = 16 / 32 -> wordwise GF(2^w)
+//   Cauchy at w = 8 -> bit-sliced GF(2^8); at w = 16 / 32 -> generic GF(2) bitmatrix
+//   liberation family -> generic GF(2) bitmatrix; raid4 -> bytewise XOR (w unused, raid4.c)
 int kernel_kind(int method, int w) {
-  if (method == BLAUM_ROTH || method == LIBERATION || method == LIBER8TION)
-    return lsec::bitmatrix_w_supported(w) ? KBITMATRIX : KNONE;
-  if (w != 8) return KNONE;
+  if (liberation_family(method)) return lsec::bitmatrix_w_supported(w) ? KBITMATRIX : KNONE;
+  if (method == RAID4) return KBYTEWISE;
+  const bool wide = (w == 16 || w == 32);
+  if (w != 8 && !wide) return KNONE;
   switch (method) {
     case REED_SOL_VAN:
     case REED_SOL_R6_OP:
-    case RAID4:
-      return KBYTEWISE;
+      return wide ? KWORDWISE : KBYTEWISE;
     case CAUCHY_ORIG:
     case CAUCHY_GOOD:
-      return KBITSLICED;
+      return wide ? KBITMATRIX : KBITSLICED;
     default:
       return KNONE;
   }
+}
+
+bool uses_u32_image(int kind) { return kind == KBITMATRIX || kind == KWORDWISE; }
+
+int *to_int_array(const lsec::gfw::Mat &m) {
+  int *a = static_cast<int *>(malloc(sizeof(int) * m.size()));
+  for (size_t i = 0; i < m.size(); ++i) a[i] = static_cast<int>(m[i]);
+  return a;
+}
+
+// word image of an R x K GF(2^w) matrix for k_gfw_wordwise: [(r*K + j)*w + b] = M[r][j] * x^b
+std::vector<uint32_t> word_image(const lsec::gfw::Mat &mat, int rows, int cols, int w) {
+  std::vector<uint32_t> img(static_cast<size_t>(rows) * cols * w);
+  for (int i = 0; i < rows * cols; ++i) lsec::make_word_cell(mat[i], w, &img[static_cast<size_t>(i) * w]);
+  return img;
+}
+
+// bitmatrix row masks for the generic bitmatrix kernel: word [(r*w+l)*k + j], bit x = B[r*w+l][j*w+x]
+std::vector<uint32_t> bitmatrix_masks(const int *bm, int k, int m, int w) {
+  std::vector<uint32_t> mk(static_cast<size_t>(m) * w * k, 0u);
+  for (int row = 0; row < m * w; ++row)
+    for (int j = 0; j < k; ++j)
+      for (int x = 0; x < w; ++x)
+        if (bm[static_cast<size_t>(row) * k * w + j * w + x]) mk[static_cast<size_t>(row) * k + j] |= 1u << x;
+  return mk;
 }
 
 int *to_int_array(const lsec::gf8::Mat &m) {
@@ -151,21 +185,38 @@ int form_matrices(lio_erasure_plan_t *p, bool with_schedule) {
     case REED_SOL_VAN:
     case REED_SOL_R6_OP: {
       if (!p->encode_matrix) {
-        const bool ok = (w == 8) && (p->method == REED_SOL_VAN ? lsec::gf8::reed_sol_vandermonde(k, m, mat)
-                                                               : lsec::gf8::reed_sol_r6(k, mat));
-        if (!ok) return fail("cannot form %s matrix for k=%d m=%d w=%d", JE_method[p->method], k, m, w);
-        p->encode_matrix = to_int_array(mat);
+        const bool r6 = p->method == REED_SOL_R6_OP;
+        if (w == 8) {
+          if (!(r6 ? lsec::gf8::reed_sol_r6(k, mat) : lsec::gf8::reed_sol_vandermonde(k, m, mat)))
+            return fail("cannot form %s matrix for k=%d m=%d w=%d", JE_method[p->method], k, m, w);
+          p->encode_matrix = to_int_array(mat);
+        } else {
+          lsec::gfw::Mat wm;
+          const bool ok = (w == 16 || w == 32) &&
+                          (r6 ? lsec::gfw::reed_sol_r6(k, w, wm) : lsec::gfw::reed_sol_vandermonde(k, m, w, wm));
+          if (!ok) return fail("cannot form %s matrix for k=%d m=%d w=%d", JE_method[p->method], k, m, w);
+          p->encode_matrix = to_int_array(wm);
+        }
       }
       break;
     }
     case CAUCHY_ORIG:
     case CAUCHY_GOOD: {
       if (!p->encode_matrix) {
-        const bool ok = (w == 8) && (p->method == CAUCHY_ORIG ? lsec::gf8::cauchy_original(k, m, mat)
-                                                              : lsec::gf8::cauchy_good(k, m, mat));
-        if (!ok) return fail("cannot form %s matrix for k=%d m=%d w=%d", JE_method[p->method], k, m, w);
-        p->encode_matrix = to_int_array(mat);
-        p->encode_bitmatrix = to_int_array(lsec::gf8::to_bitmatrix(k, m, mat));
+        const bool orig = p->method == CAUCHY_ORIG;
+        if (w == 8) {
+          if (!(orig ? lsec::gf8::cauchy_original(k, m, mat) : lsec::gf8::cauchy_good(k, m, mat)))
+            return fail("cannot form %s matrix for k=%d m=%d w=%d", JE_method[p->method], k, m, w);
+          p->encode_matrix = to_int_array(mat);
+          p->encode_bitmatrix = to_int_array(lsec::gf8::to_bitmatrix(k, m, mat));
+        } else {
+          lsec::gfw::Mat wm;
+          const bool ok = (w == 16 || w == 32) &&
+                          (orig ? lsec::gfw::cauchy_original(k, m, w, wm) : lsec::gfw::cauchy_good(k, m, w, wm));
+          if (!ok) return fail("cannot form %s matrix for k=%d m=%d w=%d", JE_method[p->method], k, m, w);
+          p->encode_matrix = to_int_array(wm);
+          p->encode_bitmatrix = to_int_array(lsec::gfw::to_bitmatrix(k, m, w, wm));
+        }
       }
       if (with_schedule && !p->encode_schedule) {
         std::vector<int> bm(p->encode_bitmatrix, p->encode_bitmatrix + static_cast<size_t>(k) * m * w * w);
@@ -187,25 +238,27 @@ int form_matrices(lio_erasure_plan_t *p, bool with_schedule) {
         std::vector<int> bm(p->encode_bitmatrix, p->encode_bitmatrix + static_cast<size_t>(k) * m * w * w);
         p->encode_schedule = schedule_array(lsec::gf8::smart_schedule(k, m, w, bm));
       }
-      if (!e->impl->coding_ready) {
-        // row masks for the generic bitmatrix kernel: word [(r*w+l)*k + j], bit x = B[r*w+l][j*w+x]
-        auto &mk = e->impl->enc_masks;
-        mk.assign(static_cast<size_t>(m) * w * k, 0u);
-        for (int row = 0; row < m * w; ++row)
-          for (int j = 0; j < k; ++j)
-            for (int x = 0; x < w; ++x)
-              if (p->encode_bitmatrix[static_cast<size_t>(row) * k * w + j * w + x]) mk[static_cast<size_t>(row) * k + j] |= 1u << x;
-        e->impl->coding_ready = true;
-      }
       break;
     }
     default:
       return fail("invalid method %d", p->method);
   }
-  if (p->encode_matrix && !e->impl->coding_ready) {
+  if (e->impl->coding_ready) return 0;
+  const int kind = kernel_kind(p->method, w);
+  if (kind == KBITMATRIX) {
+    if (!p->encode_bitmatrix) return 0;
+    e->impl->enc_masks = bitmatrix_masks(p->encode_bitmatrix, k, m, w);
+    e->impl->coding_ready = true;
+  } else if (p->encode_matrix) {
     const int rows = (p->method == REED_SOL_R6_OP) ? 2 : m;
-    e->impl->coding.resize(static_cast<size_t>(rows) * k);
-    for (size_t i = 0; i < e->impl->coding.size(); ++i) e->impl->coding[i] = static_cast<uint8_t>(p->encode_matrix[i]);
+    if (kind == KWORDWISE) {
+      e->impl->coding_w.resize(static_cast<size_t>(rows) * k);
+      for (size_t i = 0; i < e->impl->coding_w.size(); ++i) e->impl->coding_w[i] = static_cast<uint32_t>(p->encode_matrix[i]);
+      e->impl->enc_masks = word_image(e->impl->coding_w, rows, k, w);
+    } else {
+      e->impl->coding.resize(static_cast<size_t>(rows) * k);
+      for (size_t i = 0; i < e->impl->coding.size(); ++i) e->impl->coding[i] = static_cast<uint8_t>(p->encode_matrix[i]);
+    }
     e->impl->coding_ready = true;
   }
   return 0;
@@ -255,7 +308,9 @@ int upload_cells(const std::vector<CoefCell> &h, CoefCell **out) {
 
 // output rows of the encode image (m; 2 for r6, 1 for raid4)
 int encode_rows(const PlanExt *e) {
-  if (kernel_kind(e->pub.method, e->pub.w) == KBITMATRIX) return e->pub.parity_strips;
+  const int kind = kernel_kind(e->pub.method, e->pub.w);
+  if (kind == KBITMATRIX) return e->pub.parity_strips;
+  if (kind == KWORDWISE) return static_cast<int>(e->impl->coding_w.size()) / e->pub.data_strips;
   return static_cast<int>(e->impl->coding.size()) / e->pub.data_strips;
 }
 
@@ -277,7 +332,7 @@ int encode_cells(PlanExt *e, const void **out) {
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(e->impl->mu);
-  if (kernel_kind(e->pub.method, e->pub.w) == KBITMATRIX) {
+  if (uses_u32_image(kernel_kind(e->pub.method, e->pub.w))) {
     auto it = e->impl->enc_dev_masks.find(dev);
     if (it == e->impl->enc_dev_masks.end()) {
       uint32_t *d = nullptr;
@@ -330,12 +385,21 @@ int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, con
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(e->impl->mu);
-  const bool bitm = kernel_kind(e->pub.method, e->pub.w) == KBITMATRIX;
+  const int kind = kernel_kind(e->pub.method, e->pub.w);
+  const bool bitm = uses_u32_image(kind);
   auto it = e->impl->decode_cache.find(ids);
   if (it == e->impl->decode_cache.end()) {
     DecodeEntry ent;
     const int k = e->pub.data_strips;
-    if (bitm) {
+    if (kind == KWORDWISE) {
+      const int w = e->pub.w;
+      const int m = static_cast<int>(e->impl->coding_w.size()) / k;
+      lsec::gfw::DecodePlan wp;
+      if (!lsec::gfw::make_decode(k, m, w, e->impl->coding_w, ids, wp)) return fail("decoding matrix is singular");
+      ent.dp.survivors = wp.survivors;
+      ent.dp.erased = wp.erased;
+      ent.masks = word_image(wp.rows, static_cast<int>(wp.erased.size()), k, w);
+    } else if (kind == KBITMATRIX) {
       const lio_erasure_plan_t *p = &e->pub;
       std::vector<int> bm(p->encode_bitmatrix, p->encode_bitmatrix + static_cast<size_t>(k) * p->parity_strips * p->w * p->w);
       if (!lsec::gf8::make_bit_decode(k, p->parity_strips, p->w, bm, ids, ent.dp, ent.masks))
@@ -384,7 +448,7 @@ int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
     if (p->packet_size <= 0 || p->packet_size % 4 != 0 || block_size % sp != 0)
       return fail("block_size %lld is not a multiple of w*packet_size = %lld", block_size, sp);
   }
-  if (kind == KBITMATRIX && m != 2) return fail("%s needs m == 2", JE_method[p->method]);
+  if (liberation_family(p->method) && m != 2) return fail("%s needs m == 2", JE_method[p->method]);
   return 0;
 }
 
@@ -399,7 +463,7 @@ int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in,
     std::memset(&a, 0, sizeof(a));
     a.K = K;
     a.R = std::min(rmax, R - r0);
-    if (kind == KBITMATRIX) {
+    if (uses_u32_image(kind)) {  // both images hold w words per (row, input) in row-major order
       a.masks = static_cast<const uint32_t *>(image) + static_cast<size_t>(r0) * w * K;
       a.w = w;
     } else {
@@ -419,6 +483,7 @@ int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in,
       for (int r = 0; r < b.R; ++r) b.out[r].base = out[r0 + r].base + static_cast<uint64_t>(s0) * out[r0 + r].stride;
       const hipError_t err = kind == KBYTEWISE    ? lsec::launch_bytewise(b, st)
                              : kind == KBITMATRIX ? lsec::launch_bitmatrix(b, st)
+                             : kind == KWORDWISE  ? lsec::launch_wordwise(b, st)
                                                   : lsec::launch_bitsliced(b, st);
       if (err != hipSuccess) return fail("kernel launch failed: %s", hipGetErrorString(err));
     }
@@ -683,7 +748,8 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   const size_t per_col = static_cast<size_t>(nin + nout);  // staging bytes per column byte
   long long cb = C;
   if (per_col * C > budget / 2) {
-    const long long align = kind == KBITSLICED ? 8LL * p->packet_size : 8192;
+    // packet codes must cut at super-packet boundaries (w * P bytes)
+    const long long align = (kind == KBITSLICED || kind == KBITMATRIX) ? static_cast<long long>(p->w) * p->packet_size : 8192;
     cb = static_cast<long long>(budget / 2 / per_col) / align * align;
     if (cb < align) cb = align;
     if (cb >= C) cb = C;
@@ -835,6 +901,273 @@ hipStream_t thread_stream() {
   return s;
 }
 
+// ---------------------------------------------------------------- request coalescing
+// The unmodified segment driver calls encode_block / decode_block once per stripe, from up
+// to 300 gop pool threads at once (segment/jerasure.c:1847, :245, :1937; lio_config.c:87).
+// One H2D + kernel + D2H round trip per 16 KiB stripe would leave the GPU idle between tiny
+// transfers, so small host-memory calls are handed to a per-device dispatcher thread that
+// coalesces everything queued at that moment: requests with the same matrix image and
+// geometry share ONE staging region, ONE H2D, ONE kernel launch and ONE D2H (group commit).
+// Two staging slots alternate so packing batch n+1 overlaps the GPU work of batch n.
+struct HostReq {
+  char **ptrs = nullptr;
+  int nstripes = 0, km = 0, kind = 0, packet = 0, w = 8;
+  long long C = 0;
+  std::vector<int> in_ids, out_ids;
+  const void *image = nullptr;
+  int rc = 0;
+  std::string err;
+  bool done = false;
+  std::mutex mu;
+  std::condition_variable cv;
+  size_t bytes() const { return static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()) * C; }
+  bool same_group(const HostReq &o) const {
+    return image == o.image && kind == o.kind && C == o.C && packet == o.packet && w == o.w && in_ids.size() == o.in_ids.size() &&
+           out_ids.size() == o.out_ids.size();
+  }
+};
+
+size_t coalesce_limit() {  // per-request bytes below which calls go through the dispatcher
+  static size_t b = [] {
+    const char *s = getenv("LSEC_COALESCE_MB");
+    return static_cast<size_t>(std::max(0L, s ? atol(s) : 16)) << 20;
+  }();
+  return b;
+}
+
+class Dispatcher {
+ public:
+  static Dispatcher *for_device(int dev) {
+    static std::mutex mu;
+    static std::map<int, Dispatcher *> all;  // intentionally leaked: lives until exit
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = all.find(dev);
+    if (it != all.end()) return it->second;
+    Dispatcher *d = new Dispatcher(dev);
+    all[dev] = d;
+    return d;
+  }
+
+  int run(HostReq &r) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.push_back(&r);
+    }
+    cv_.notify_one();
+    std::unique_lock<std::mutex> lk(r.mu);
+    r.cv.wait(lk, [&] { return r.done; });
+    if (r.rc) tl_err = r.err;
+    return r.rc;
+  }
+
+ private:
+  struct Group {
+    std::vector<HostReq *> reqs;
+    std::vector<int> first;  // stripe offset of each request inside the group
+    int nstripes = 0;
+    size_t off = 0;          // byte offset of the group inside the slot
+  };
+  struct Slot {
+    char *d = nullptr, *h = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+    std::vector<Group> groups;
+    std::string err;
+  };
+
+  static constexpr size_t kBatchBudget = 96u << 20;  // bytes packed per dispatcher batch
+
+  explicit Dispatcher(int dev) : dev_(dev) { std::thread([this] { loop(); }).detach(); }
+
+  static size_t group_bytes(const Group &g) {
+    const HostReq &r = *g.reqs[0];
+    return static_cast<size_t>(g.nstripes) * (r.in_ids.size() + r.out_ids.size()) * r.C;
+  }
+
+  void finish(Slot &sl) {
+    if (sl.groups.empty()) return;
+    std::string err = sl.err;
+    if (err.empty() && hipEventSynchronize(sl.done) != hipSuccess) err = "dispatcher: event sync failed";
+    std::vector<CopyJob> jobs;
+    if (err.empty()) {
+      for (const Group &g : sl.groups) {
+        const HostReq &r0 = *g.reqs[0];
+        const size_t C = static_cast<size_t>(r0.C), nin = r0.in_ids.size(), nout = r0.out_ids.size();
+        const char *outb = sl.h + g.off + static_cast<size_t>(g.nstripes) * nin * C;
+        for (size_t q = 0; q < g.reqs.size(); ++q) {
+          const HostReq &r = *g.reqs[q];
+          for (int s = 0; s < r.nstripes; ++s)
+            for (size_t o = 0; o < nout; ++o)
+              jobs.push_back({r.ptrs[static_cast<size_t>(s) * r.km + r.out_ids[o]],
+                              outb + ((static_cast<size_t>(g.first[q]) + s) * nout + o) * C, C});
+        }
+      }
+      CopyPool::get().run(jobs);
+    }
+    for (const Group &g : sl.groups)
+      for (HostReq *r : g.reqs) {
+        std::lock_guard<std::mutex> lk(r->mu);
+        r->rc = err.empty() ? 0 : -1;
+        r->err = err;
+        r->done = true;
+        r->cv.notify_all();
+      }
+    sl.groups.clear();
+    sl.err.clear();
+  }
+
+  // pack + enqueue one batch into `sl`; errors are recorded in sl.err (reported at finish)
+  void launch(Slot &sl, std::vector<HostReq *> &batch) {
+    for (HostReq *r : batch) {  // group compatible requests
+      Group *g = nullptr;
+      for (Group &x : sl.groups)
+        if (x.reqs[0]->same_group(*r)) { g = &x; break; }
+      if (!g) {
+        sl.groups.emplace_back();
+        g = &sl.groups.back();
+      }
+      g->reqs.push_back(r);
+      g->first.push_back(g->nstripes);
+      g->nstripes += r->nstripes;
+    }
+    size_t total = 0;
+    for (Group &g : sl.groups) {
+      g.off = total;
+      total += (group_bytes(g) + 255) & ~static_cast<size_t>(255);
+    }
+    auto hip_err = [&](hipError_t e, const char *what) {
+      if (e != hipSuccess && sl.err.empty()) sl.err = std::string("dispatcher: ") + what + ": " + hipGetErrorString(e);
+      return e == hipSuccess;
+    };
+    if (sl.cap < total) {
+      if (sl.d) (void)hipFree(sl.d);
+      if (sl.h) (void)hipHostFree(sl.h);
+      sl.d = sl.h = nullptr;
+      // grow geometrically up to the batch budget: pinning a fresh region costs milliseconds
+      // per call, so creeping batch sizes must not re-pin on every growth step
+      const size_t cap = std::max({total, std::min(2 * sl.cap, kBatchBudget + (1u << 20)), size_t(32u << 20)});
+      sl.cap = 0;
+      if (!hip_err(hipMalloc(&sl.d, cap), "hipMalloc") ||
+          !hip_err(hipHostMalloc(reinterpret_cast<void **>(&sl.h), cap, hipHostMallocDefault), "hipHostMalloc"))
+        return;
+      sl.cap = cap;
+    }
+    std::vector<CopyJob> jobs;
+    for (const Group &g : sl.groups) {
+      const HostReq &r0 = *g.reqs[0];
+      const size_t C = static_cast<size_t>(r0.C), nin = r0.in_ids.size();
+      for (size_t q = 0; q < g.reqs.size(); ++q) {
+        const HostReq &r = *g.reqs[q];
+        for (int s = 0; s < r.nstripes; ++s)
+          for (size_t j = 0; j < nin; ++j)
+            jobs.push_back({sl.h + g.off + ((static_cast<size_t>(g.first[q]) + s) * nin + j) * C,
+                            r.ptrs[static_cast<size_t>(s) * r.km + r.in_ids[j]], C});
+      }
+    }
+    CopyPool::get().run(jobs);
+    for (const Group &g : sl.groups) {
+      const HostReq &r0 = *g.reqs[0];
+      const size_t C = static_cast<size_t>(r0.C);
+      const int nin = static_cast<int>(r0.in_ids.size()), nout = static_cast<int>(r0.out_ids.size());
+      const size_t in_bytes = static_cast<size_t>(g.nstripes) * nin * C;
+      char *dbase = sl.d + g.off;
+      if (!hip_err(hipMemcpyAsync(dbase, sl.h + g.off, in_bytes, hipMemcpyHostToDevice, s_in_), "H2D")) return;
+      if (!hip_err(hipEventRecord(in_done_, s_in_), "event") || !hip_err(hipStreamWaitEvent(s_out_, in_done_, 0), "wait"))
+        return;
+      ShardRef in[lsec::kMaxK], out[64];
+      for (int j = 0; j < nin; ++j)
+        in[j] = {reinterpret_cast<uint64_t>(dbase) + static_cast<uint64_t>(j) * C, static_cast<int64_t>(nin * C)};
+      for (int o = 0; o < nout; ++o)
+        out[o] = {reinterpret_cast<uint64_t>(dbase) + in_bytes + static_cast<uint64_t>(o) * C, static_cast<int64_t>(nout * C)};
+      if (enqueue_apply(r0.kind, r0.image, nin, nout, in, out, g.nstripes, r0.C, r0.packet, s_out_, r0.w) != 0) {
+        if (sl.err.empty()) sl.err = tl_err;
+        return;
+      }
+      if (!hip_err(hipMemcpyAsync(sl.h + g.off + in_bytes, dbase + in_bytes, static_cast<size_t>(g.nstripes) * nout * C,
+                                  hipMemcpyDeviceToHost, s_out_), "D2H"))
+        return;
+    }
+    hip_err(hipEventRecord(sl.done, s_out_), "event");
+  }
+
+  void loop() {
+    if (hipSetDevice(dev_) != hipSuccess || hipStreamCreateWithFlags(&s_in_, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&s_out_, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&in_done_, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&slot_[0].done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&slot_[1].done, hipEventDisableTiming) != hipSuccess) {
+      broken_ = "dispatcher: cannot create HIP streams/events";
+    }
+    int cur = 0;
+    for (;;) {
+      std::vector<HostReq *> batch;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        const bool pending = !slot_[cur ^ 1].groups.empty();
+        if (!pending) cv_.wait(lk, [&] { return !q_.empty(); });
+        size_t bytes = 0;
+        while (!q_.empty() && (batch.empty() || bytes + q_.front()->bytes() <= kBatchBudget)) {
+          bytes += q_.front()->bytes();
+          batch.push_back(q_.front());
+          q_.pop_front();
+        }
+      }
+      if (!batch.empty()) {
+        if (!broken_.empty()) slot_[cur].err = broken_;
+        else launch(slot_[cur], batch);
+        if (slot_[cur].groups.empty()) {  // launch failed before grouping
+          for (HostReq *r : batch) {
+            std::lock_guard<std::mutex> lk(r->mu);
+            r->rc = -1;
+            r->err = slot_[cur].err.empty() ? broken_ : slot_[cur].err;
+            r->done = true;
+            r->cv.notify_all();
+          }
+          slot_[cur].err.clear();
+        }
+      }
+      finish(slot_[cur ^ 1]);  // complete the previous batch while this one runs
+      cur ^= 1;
+    }
+  }
+
+  int dev_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<HostReq *> q_;
+  Slot slot_[2];
+  hipStream_t s_in_ = nullptr, s_out_ = nullptr;
+  hipEvent_t in_done_ = nullptr;
+  std::string broken_;
+};
+
+int run_coalesced(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
+                  const std::vector<int> &out_ids, const void *image, int kind) {
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  HostReq r;
+  r.ptrs = ptrs;
+  r.nstripes = nstripes;
+  r.km = e->pub.data_strips + e->pub.parity_strips;
+  r.C = C;
+  r.in_ids = in_ids;
+  r.out_ids = out_ids;
+  r.image = image;
+  r.kind = kind;
+  r.packet = e->pub.packet_size;
+  r.w = e->pub.w;
+  return Dispatcher::for_device(dev)->run(r);
+}
+
+// host-memory batches: small ones are coalesced with concurrent callers, large ones stream
+// through their own staging pipeline
+int run_host_auto(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
+                  const std::vector<int> &out_ids, const void *image, int kind) {
+  const size_t bytes = static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()) * C;
+  if (bytes <= coalesce_limit()) return run_coalesced(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
+  return run_host(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
+}
+
 int encode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C) {
   lio_erasure_plan_t *p = &e->pub;
   if (!ptrs) return fail("ptrs is NULL");
@@ -855,7 +1188,7 @@ int encode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C) {
   std::vector<int> in_ids(k), out_ids(R);
   for (int j = 0; j < k; ++j) in_ids[j] = j;
   for (int r = 0; r < R; ++r) out_ids[r] = k + r;
-  return run_host(e, ptrs, nstripes, C, in_ids, out_ids, cells, kernel_kind(p->method, p->w));
+  return run_host_auto(e, ptrs, nstripes, C, in_ids, out_ids, cells, kernel_kind(p->method, p->w));
 }
 
 int decode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C, const int *erasures) {
@@ -879,7 +1212,7 @@ int decode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C, cons
   DecodeEntry *ent = nullptr;
   const void *cells = nullptr;
   if (decode_entry(e, ids, &ent, &cells)) return -1;
-  return run_host(e, ptrs, nstripes, C, ent->dp.survivors, ent->dp.erased, cells, kernel_kind(p->method, p->w));
+  return run_host_auto(e, ptrs, nstripes, C, ent->dp.survivors, ent->dp.erased, cells, kernel_kind(p->method, p->w));
 }
 
 int encode_stripes_magic_impl(PlanExt *e, char **ptrs, int nstripes, long long C, uint8_t *magic) {
@@ -967,6 +1300,10 @@ void parallel_copy(std::vector<HostCopy> &jobs) {
   j.reserve(jobs.size());
   for (const HostCopy &h : jobs) j.push_back({h.dst, h.src, h.bytes});
   CopyPool::get().run(j);
+}
+
+void make_word_cell(uint32_t c, int w, uint32_t *out) {
+  for (int b = 0; b < w; ++b, c = gfw::times_x(c, w)) out[b] = (w == 16) ? (c | (c << 16)) : c;
 }
 
 void make_cell(uint8_t c, CoefCell &cell) {
@@ -1321,8 +1658,42 @@ int lsec_encode_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, 
   PlanExt *e = ext_of(plan);
   if (!e) return fail("not an lstore_ec plan");
   if (!shards || !magic) return fail("shards / magic is NULL");
-  if (encode_dev(e, shards, nstripes, block_size, static_cast<hipStream_t>(stream))) return -1;
-  return magic_dev_impl(e, shards, nstripes, block_size, static_cast<uint8_t *>(magic), static_cast<hipStream_t>(stream));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int k = plan->data_strips, m = plan->parity_strips;
+  if (kernel_kind(plan->method, plan->w) == KBYTEWISE && m <= 8 && !check_geometry(plan, block_size) &&
+      k + m <= lsec::kMaxMagicShards) {
+    // one pass: the encode kernel also accumulates the magic of the k inputs and m outputs
+    if (nstripes <= 0 || block_size == 0) return 0;
+    const void *cells = nullptr;
+    if (encode_cells(e, &cells)) return -1;
+    if (encode_rows(e) != m) return fail("stripe magic needs m parity rows");
+    unsigned long long *acc = nullptr;
+    HIP_OK(hipMallocAsync(reinterpret_cast<void **>(&acc), 16ull * nstripes, st));
+    HIP_OK(hipMemsetAsync(acc, 0, 16ull * nstripes, st));
+    lsec::ApplyArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.cells = static_cast<const CoefCell *>(cells);
+    a.K = k;
+    a.R = m;
+    a.size = block_size;
+    const int per = static_cast<int>(std::max(1LL, (1LL << 30) / std::max(1LL, block_size / 8192 + 1)));
+    for (int s0 = 0; s0 < nstripes; s0 += per) {
+      a.nstripes = std::min(per, nstripes - s0);
+      a.magic_acc = acc + 2ull * s0;
+      for (int j = 0; j < k; ++j)
+        a.in[j] = {reinterpret_cast<uint64_t>(shards[j].base) + static_cast<uint64_t>(s0) * shards[j].stride, shards[j].stride};
+      for (int r = 0; r < m; ++r)
+        a.out[r] = {reinterpret_cast<uint64_t>(shards[k + r].base) + static_cast<uint64_t>(s0) * shards[k + r].stride,
+                    shards[k + r].stride};
+      HIP_OK(lsec::launch_bytewise_magic(a, st));
+    }
+    HIP_OK(lsec::launch_magic_finalize(acc, nstripes, static_cast<int64_t>(k + m) * block_size,
+                                       static_cast<uint8_t *>(magic), st));
+    HIP_OK(hipFreeAsync(acc, st));
+    return 0;
+  }
+  if (encode_dev(e, shards, nstripes, block_size, st)) return -1;
+  return magic_dev_impl(e, shards, nstripes, block_size, static_cast<uint8_t *>(magic), st);
 }
 
 int lsec_prepare_decode(lio_erasure_plan_t *plan, const int *erasures) {

@@ -48,8 +48,11 @@ struct ApplyArgs {
   int nstripes;
   int packet;             // bitsliced / bitmatrix: packet size P (bytes)
   int64_t size;           // bytes per shard (chunk C)
-  const uint32_t *masks;  // bitmatrix only: (R*w) x K words, bit x of [(r*w+l)*K + j] = B[r*w+l][j*w+x]
-  int w;                  // bitmatrix only: packets per super-packet
+  const uint32_t *masks;  // bitmatrix: (R*w) x K words, bit x of [(r*w+l)*K + j] = B[r*w+l][j*w+x]
+                          // wordwise: R x K x w products, [(r*K + j)*w + b] = c_rj * x^b
+  int w;                  // bitmatrix: packets per super-packet; wordwise: field width (16 / 32)
+  unsigned long long *magic_acc;  // bytewise encode only: fused stripe magic over the K inputs then the
+                                  // R outputs (2 x u64 per stripe, zeroed), see MagicArgs
   ShardRef in[kMaxK];
   ShardRef out[kMaxR];
 };
@@ -84,11 +87,17 @@ void make_cell(uint8_t c, CoefCell &cell);
 
 // Launchers (return hipError_t of the launch).  grid_blocks <= 0 picks a default.
 hipError_t launch_bytewise(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
+// encode + stripe magic in one pass (a.magic_acc != nullptr; checksum order = inputs, outputs)
+hipError_t launch_bytewise_magic(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
 hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
-// generic GF(2) bitmatrix codes (liberation / blaum_roth / liber8tion, liberation.c): any w in
-// kBitmatrixW, R <= 2 (these codes have m = 2)
+// generic GF(2) bitmatrix codes (liberation / blaum_roth / liber8tion, liberation.c; Cauchy at
+// w = 16 / 32): any w in LSEC_BITMATRIX_W, R <= 2 per launch
 hipError_t launch_bitmatrix(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
 bool bitmatrix_w_supported(int w);
+// matrix codes over GF(2^16) / GF(2^32) (a.w), little-endian words, R <= 8
+hipError_t launch_wordwise(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
+// host helper: the w products c * x^b (b = 0..w-1) of a wordwise cell, replicated for w = 16
+void make_word_cell(uint32_t c, int w, uint32_t *out);
 
 // Variant selection knobs for experiments: 0 = default
 void set_kernel_variant(int bytewise_variant, int bitsliced_variant);

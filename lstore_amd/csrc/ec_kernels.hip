@@ -65,6 +65,16 @@ hipError_t launch_bytewise(const ApplyArgs &a, hipStream_t st, int grid_blocks) 
   return by_r(a.R, [&](auto r) { return dispatch_bytewise<decltype(r)::value>(a, st, grid, shape); });
 }
 
+hipError_t launch_bytewise_magic(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
+  if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > 8 || a.size % 8 != 0 || !a.magic_acc) return hipErrorInvalidValue;
+  if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
+  const uint64_t tile = static_cast<uint64_t>(kBlock) * 16 * 2;
+  const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
+  if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
+  const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);
+  return by_r(a.R, [&](auto r) { return dispatch_bytewise_magic<decltype(r)::value>(a, st, grid); });
+}
+
 hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
   if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > 8 || a.packet <= 0 || a.packet % 4 != 0 ||
       a.size % (8LL * a.packet) != 0)
@@ -103,36 +113,19 @@ hipError_t launch_bitmatrix(const ApplyArgs &a, hipStream_t st, int grid_blocks)
   return by_r(a.R, [&](auto r) { return dispatch_bitmatrix<decltype(r)::value>(a, st, grid); });
 }
 
+hipError_t launch_wordwise(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
+  if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > 8 || (a.w != 16 && a.w != 32) || !a.masks || a.size % 8 != 0)
+    return hipErrorInvalidValue;
+  if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
+  const uint64_t tile = kBlock * (a.w == 16 ? 16ull : 8ull);  // bytes per shard per tile (VW = 4 / 2 dwords per lane)
+  const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
+  if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
+  const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);
+  return by_r(a.R, [&](auto r) { return dispatch_wordwise<decltype(r)::value>(a, st, grid); });
+}
+
 // ------------------------------------------------------------------ stripe magic (adler32)
 namespace {
-
-constexpr uint32_t kAdlerMod = 65521;
-
-__device__ __forceinline__ void adler_add16(u32x4 v, uint64_t len_minus_pos, uint64_t &a_sum, uint64_t &b_sum) {
-  // S = sum of the 16 bytes, U = sum t*b_t (t = 0..15) via packed byte dot products
-  uint32_t S = 0, U = 0;
-  S = __builtin_amdgcn_udot4(v.x, 0x01010101u, S, false);
-  S = __builtin_amdgcn_udot4(v.y, 0x01010101u, S, false);
-  S = __builtin_amdgcn_udot4(v.z, 0x01010101u, S, false);
-  S = __builtin_amdgcn_udot4(v.w, 0x01010101u, S, false);
-  U = __builtin_amdgcn_udot4(v.x, 0x03020100u, U, false);
-  U = __builtin_amdgcn_udot4(v.y, 0x07060504u, U, false);
-  U = __builtin_amdgcn_udot4(v.z, 0x0B0A0908u, U, false);
-  U = __builtin_amdgcn_udot4(v.w, 0x0F0E0D0Cu, U, false);
-  a_sum += S;
-  b_sum += len_minus_pos * S - U;   // sum_t (L - p - t) b_t, every term >= 0
-}
-
-__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *lds) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
-  __syncthreads();
-  uint32_t t = 0;
-  if (threadIdx.x == 0)
-    for (int w = 0; w < kBlock / 64; ++w) t += lds[w];
-  __syncthreads();
-  return t;
-}
 
 // one block per (stripe, 8 KiB column tile); each lane reads 16 B x 2 of every shard
 __global__ __launch_bounds__(kBlock) void k_stripe_magic(MagicArgs a) {
@@ -159,7 +152,7 @@ __global__ __launch_bounds__(kBlock) void k_stripe_magic(MagicArgs a) {
           v.x = h.x;
           v.y = h.y;
         }
-        adler_add16(v, L - static_cast<uint64_t>(i * a.chunk + a.col0 + o), as, bs);
+        adler_add(v, L - static_cast<uint64_t>(i * a.chunk + a.col0 + o), as, bs);
       }
     }
     const uint32_t am = block_sum(static_cast<uint32_t>(as % kAdlerMod), red);

@@ -85,6 +85,35 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
   return xcd * per + min(xcd, rem) + (b >> 3);
 }
 
+// ------------------------------------------------------------------ adler32 partial sums
+constexpr uint32_t kAdlerMod = 65521;
+
+template <typename V>
+__device__ __forceinline__ void adler_add(V v, uint64_t len_minus_pos, uint64_t &a_sum, uint64_t &b_sum) {
+  // S = sum of the 16 bytes, U = sum t*b_t (t = 0..15) via packed byte dot products
+  constexpr int N = sizeof(V) / 4;
+  uint32_t S = 0, U = 0;
+#pragma unroll
+  for (int e = 0; e < N; ++e) {
+    const uint32_t x = reinterpret_cast<const uint32_t *>(&v)[e];
+    S = __builtin_amdgcn_udot4(x, 0x01010101u, S, false);
+    U = __builtin_amdgcn_udot4(x, 0x03020100u + 0x04040404u * e, U, false);
+  }
+  a_sum += S;
+  b_sum += len_minus_pos * S - U;   // sum_t (L - p - t) b_t, every term >= 0
+}
+
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *lds) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < kBlock / 64; ++w) t += lds[w];
+  __syncthreads();
+  return t;
+}
+
 // Per-lane work unit of the bytewise kernel: VW dwords (16 B for VW = 4, 8 B for VW = 2) per
 // step, IT steps kBlock*4*VW bytes apart; a tile is kBlock*4*VW*IT bytes of every shard.
 template <int IT, int VW>
@@ -123,10 +152,47 @@ __device__ __forceinline__ void bw_accumulate(typename VecT<VW>::type (&acc)[IT]
   }
 }
 
+// fused stripe magic: every lane adds its bytes' position-weighted sums, the block reduces
+// them and adds one pair per tile into the stripe's accumulator
+template <int R, int IT, int VW>
+__device__ __forceinline__ void bw_magic(const ApplyArgs &a, uint32_t s, int64_t off0, int K,
+                                         const typename VecT<VW>::type (*v)[IT], int nv, int j0,
+                                         uint64_t &as, uint64_t &bs) {
+  constexpr int kStep = kBlock * 4 * VW;
+  const uint64_t L = static_cast<uint64_t>(K + R) * a.size;
+  for (int jj = 0; jj < nv; ++jj)
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+      adler_add(v[jj][it], L - static_cast<uint64_t>((j0 + jj) * a.size + off0 + it * kStep), as, bs);
+}
+
+template <int R, int IT, int VW>
+__device__ __forceinline__ void bw_magic_out(const ApplyArgs &a, int64_t off0, int K,
+                                             const typename VecT<VW>::type (&acc)[IT][R], uint64_t &as, uint64_t &bs) {
+  constexpr int kStep = kBlock * 4 * VW;
+  const uint64_t L = static_cast<uint64_t>(K + R) * a.size;
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+      adler_add(acc[it][r], L - static_cast<uint64_t>((K + r) * a.size + off0 + it * kStep), as, bs);
+}
+
+__device__ __forceinline__ void magic_commit(unsigned long long *acc, uint32_t s, uint64_t as, uint64_t bs, uint32_t *red) {
+  const uint32_t am = block_sum(static_cast<uint32_t>(as % kAdlerMod), red);
+  const uint32_t bm = block_sum(static_cast<uint32_t>(bs % kAdlerMod), red);
+  if (threadIdx.x == 0) {
+    atomicAdd(acc + 2 * s, static_cast<unsigned long long>(am));
+    atomicAdd(acc + 2 * s + 1, static_cast<unsigned long long>(bm));
+  }
+}
+
 // MINW = minimum waves per SIMD the register allocation must allow (1 = unconstrained).
-template <int R, int KC, int IT, int MINW, int VW>
+// MG = also accumulate the stripe magic of inputs + outputs (encode + je_cksum_calc fused).
+template <int R, int KC, int IT, int MINW, int VW, bool MG = false>
 __global__ __launch_bounds__(kBlock, MINW) void k_gf8_bytewise(ApplyArgs a) {
   typedef typename VecT<VW>::type V;
+  __shared__ uint32_t red[MG ? kBlock / 64 : 1];
   constexpr int kStep = BwTile<IT, VW>::kStep;
   constexpr int kTile = BwTile<IT, VW>::kBytes;
   constexpr int kLane = 4 * VW;
@@ -146,6 +212,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_gf8_bytewise(ApplyArgs a) {
     for (int it = 0; it < IT; ++it)
 #pragma unroll
       for (int r = 0; r < R; ++r) acc[it][r] = 0u;
+    uint64_t mas = 0, mbs = 0;  // fused magic partial sums (MG only)
 
     if (full) {
       if constexpr (KC > 0) {
@@ -159,6 +226,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_gf8_bytewise(ApplyArgs a) {
         }
 #pragma unroll
         for (int j = 0; j < KC; ++j) bw_accumulate<R, IT, VW>(acc, v[j], cells, K, j);
+        if constexpr (MG) bw_magic<R, IT, VW>(a, s, off0, K, v, KC, 0, mas, mbs);
       } else {
         for (int j0 = 0; j0 < K; j0 += 4) {
           V v[4][IT];
@@ -174,6 +242,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_gf8_bytewise(ApplyArgs a) {
 #pragma unroll
           for (int jj = 0; jj < 4; ++jj)
             if (jj < nj) bw_accumulate<R, IT, VW>(acc, v[jj], cells, K, j0 + jj);
+          if constexpr (MG) bw_magic<R, IT, VW>(a, s, off0, K, v, nj, j0, mas, mbs);
         }
       }
 #pragma unroll
@@ -200,6 +269,10 @@ __global__ __launch_bounds__(kBlock, MINW) void k_gf8_bytewise(ApplyArgs a) {
           }
         }
         bw_accumulate<R, IT, VW>(acc, v, cells, K, j);
+        if constexpr (MG) {
+          const V(*vv)[IT] = &v;
+          bw_magic<R, IT, VW>(a, s, off0, K, vv, 1, j, mas, mbs);
+        }
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -217,6 +290,10 @@ __global__ __launch_bounds__(kBlock, MINW) void k_gf8_bytewise(ApplyArgs a) {
           }
         }
       }
+    }
+    if constexpr (MG) {
+      bw_magic_out<R, IT, VW>(a, off0, K, acc, mas, mbs);
+      magic_commit(a.magic_acc, s, mas, mbs, red);
     }
   }
 }
@@ -340,10 +417,100 @@ __global__ __launch_bounds__(kBlock) void k_bitmatrix(ApplyArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ wordwise GF(2^16) / GF(2^32)
+// Reed-Solomon at w = 16 / 32 (jerasure_matrix_dotprod -> galois_w16/w32_region_multiply,
+// galois.c:527-604, :730-810): element t of a shard is the little-endian uint16 / uint32 at
+// byte 2t / 4t.  c*v = XOR_{b: v_b = 1} (c * x^b), so with the W products P_b = c*x^b of a
+// cell in SGPRs (image [(r*K + j)*W + b], replicated into both halves of the dword for
+// W = 16), each input dword yields W bit masks (bit b of each element smeared over the
+// element: v_pk_lshlrev_b16 + v_pk_ashrrev_i16 for two uint16 elements, v_bfe_i32 for one
+// uint32) shared by all R outputs, and each (output, input, bit) costs one v_bitop3_b32
+// (acc ^ (mask & P_b), truth table 0x78).  VALU-bound by design at W ops per dword per
+// (output, input) pair; these word sizes are off the headline configs.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+template <int W>
+__device__ __forceinline__ uint32_t bit_smear(uint32_t x, int b) {
+  if constexpr (W == 32) {
+    return static_cast<uint32_t>(static_cast<int32_t>(x << (31 - b)) >> 31);
+  } else {
+    const s16x2 v = __builtin_bit_cast(s16x2, x);
+    const s16x2 m = (v << static_cast<short>(15 - b)) >> static_cast<short>(15);
+    return __builtin_bit_cast(uint32_t, m);
+  }
+}
+
+template <int R, int W>
+__global__ __launch_bounds__(kBlock) void k_gfw_wordwise(ApplyArgs a) {
+  constexpr int VW = W == 16 ? 4 : 2;
+  typedef typename VecT<VW>::type V;
+  constexpr int kLane = 4 * VW;
+  constexpr int kTile = kBlock * kLane;
+  constexpr uint32_t kOne = W == 16 ? 0x00010001u : 1u;
+  const int K = a.K;
+  const int64_t C = a.size;
+  const uint32_t tiles_per_stripe = static_cast<uint32_t>((C + kTile - 1) / kTile);
+  const uint32_t ntiles = tiles_per_stripe * static_cast<uint32_t>(a.nstripes);
+  ConstU32 *prod = reinterpret_cast<ConstU32 *>(reinterpret_cast<uintptr_t>(a.masks));
+  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+    const uint32_t s = t / tiles_per_stripe;
+    const int64_t off = static_cast<int64_t>(t - s * tiles_per_stripe) * kTile + threadIdx.x * kLane;
+    if (off >= C) continue;
+    const bool whole = off + kLane <= C;  // C % 8 == 0: otherwise exactly 8 bytes remain
+    V acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0u;
+    for (int j = 0; j < K; ++j) {
+      const uint64_t p = a.in[j].base + s * a.in[j].stride + off;
+      V v = 0u;
+      if (whole) {
+        v = __builtin_nontemporal_load(gptr<V>(p));
+      } else {
+        const u32x2 h = *gptr<u32x2>(p);
+        v[0] = h.x;
+        v[1] = h.y;
+      }
+      V mk[W];
+#pragma unroll
+      for (int b = 0; b < W; ++b)
+#pragma unroll
+        for (int e = 0; e < VW; ++e) mk[b][e] = bit_smear<W>(v[e], b);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        ConstU32 *pc = prod + (r * K + j) * W;  // wave-uniform -> scalar loads
+        const uint32_t c0 = pc[0];
+        if (c0 == 0) continue;
+        if (c0 == kOne) {
+          acc[r] ^= v;
+          continue;
+        }
+#pragma unroll
+        for (int b = 0; b < W; ++b) {
+          const uint32_t pb = pc[b];
+#pragma unroll
+          for (int e = 0; e < VW; ++e) acc[r][e] = __builtin_amdgcn_bitop3_b32(acc[r][e], mk[b][e], pb, 0x78);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
+      if (whole) {
+        __builtin_nontemporal_store(acc[r], gptr_w<V>(q));
+      } else {
+        u32x2 h;
+        h.x = acc[r][0];
+        h.y = acc[r][1];
+        *gptr_w<u32x2>(q) = h;
+      }
+    }
+  }
+}
+
 // word sizes the liberation family can produce: primes (liberation), p-1 for prime p
-// (blaum_roth), 8 (liber8tion)
+// (blaum_roth), 8 (liber8tion); 16 and 32 for Cauchy at those word sizes
 #define LSEC_BITMATRIX_W(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(10) X(11) X(12) X(13) X(16) X(17) \
-                            X(18) X(19) X(22) X(23) X(28) X(29) X(30) X(31)
+                            X(18) X(19) X(22) X(23) X(28) X(29) X(30) X(31) X(32)
 
 // ------------------------------------------------------------------ per-R dispatch
 template <int R, int IT, int MINW, int VW>
@@ -376,6 +543,18 @@ hipError_t dispatch_bytewise(const ApplyArgs &a, hipStream_t st, int grid, int s
 }
 
 template <int R>
+hipError_t dispatch_bytewise_magic(const ApplyArgs &a, hipStream_t st, int grid) {
+  switch (a.K) {
+#define LSEC_BWM_K(KK) \
+  case KK: hipLaunchKernelGGL((k_gf8_bytewise<R, KK, 2, 1, 4, true>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    LSEC_BWM_K(4) LSEC_BWM_K(6) LSEC_BWM_K(8) LSEC_BWM_K(10) LSEC_BWM_K(12) LSEC_BWM_K(16) LSEC_BWM_K(20)
+#undef LSEC_BWM_K
+    default: hipLaunchKernelGGL((k_gf8_bytewise<R, 0, 2, 1, 4, true>), dim3(grid), dim3(kBlock), 0, st, a); break;
+  }
+  return hipGetLastError();
+}
+
+template <int R>
 hipError_t dispatch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid, int dw) {
   switch (dw) {
     case 4: hipLaunchKernelGGL((k_gf8_bitsliced<R, 0, 4>), dim3(grid), dim3(kBlock), 0, st, a); break;
@@ -401,10 +580,22 @@ hipError_t dispatch_bitmatrix(const ApplyArgs &a, hipStream_t st, int grid) {
   }
 }
 
+template <int R>
+hipError_t dispatch_wordwise(const ApplyArgs &a, hipStream_t st, int grid) {
+  switch (a.w) {
+    case 16: hipLaunchKernelGGL((k_gfw_wordwise<R, 16>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    case 32: hipLaunchKernelGGL((k_gfw_wordwise<R, 32>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 #define LSEC_DECLARE_R(RR)                                                                         \
   extern template hipError_t dispatch_bytewise<RR>(const ApplyArgs &, hipStream_t, int, int);      \
   extern template hipError_t dispatch_bitsliced<RR>(const ApplyArgs &, hipStream_t, int, int);         \
-  extern template hipError_t dispatch_bitmatrix<RR>(const ApplyArgs &, hipStream_t, int);
+  extern template hipError_t dispatch_bitmatrix<RR>(const ApplyArgs &, hipStream_t, int);           \
+  extern template hipError_t dispatch_bytewise_magic<RR>(const ApplyArgs &, hipStream_t, int);          \
+  extern template hipError_t dispatch_wordwise<RR>(const ApplyArgs &, hipStream_t, int);
 #ifndef LSEC_INSTANTIATING
 LSEC_DECLARE_R(1) LSEC_DECLARE_R(2) LSEC_DECLARE_R(3) LSEC_DECLARE_R(4)
 LSEC_DECLARE_R(5) LSEC_DECLARE_R(6) LSEC_DECLARE_R(7) LSEC_DECLARE_R(8)

@@ -11,4 +11,6 @@ namespace lsec {
 template hipError_t dispatch_bytewise<LSEC_R>(const ApplyArgs &, hipStream_t, int, int);
 template hipError_t dispatch_bitsliced<LSEC_R>(const ApplyArgs &, hipStream_t, int, int);
 template hipError_t dispatch_bitmatrix<LSEC_R>(const ApplyArgs &, hipStream_t, int);
+template hipError_t dispatch_bytewise_magic<LSEC_R>(const ApplyArgs &, hipStream_t, int);
+template hipError_t dispatch_wordwise<LSEC_R>(const ApplyArgs &, hipStream_t, int);
 }  // namespace lsec

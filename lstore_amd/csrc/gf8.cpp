@@ -424,4 +424,214 @@ std::vector<int> blaum_roth_bitmatrix(int k, int w) {
 }
 
 }  // namespace gf8
+
+// ==================================================================== GF(2^16) / GF(2^32)
+namespace gfw {
+
+namespace {
+uint64_t full_poly(int w) { return w == 16 ? 0x1100Bull : (1ull << 32) | 0x400007ull; }
+uint32_t field_mask(int w) { return w == 32 ? 0xFFFFFFFFu : (1u << w) - 1; }
+}  // namespace
+
+uint32_t mul(uint32_t a, uint32_t b, int w) {
+  if (w == 8) return gf8::mul(static_cast<uint8_t>(a), static_cast<uint8_t>(b));
+  uint64_t p = 0;  // carry-less product, then reduce from the top bit down
+  for (int i = 0; i < w; ++i)
+    if ((b >> i) & 1u) p ^= static_cast<uint64_t>(a) << i;
+  const uint64_t f = full_poly(w);
+  for (int i = 2 * w - 2; i >= w; --i)
+    if ((p >> i) & 1u) p ^= f << (i - w);
+  return static_cast<uint32_t>(p) & field_mask(w);
+}
+
+uint32_t times_x(uint32_t a, int w) { return mul(a, 2, w); }
+
+uint32_t inv(uint32_t a, int w) {
+  if (w == 8) return gf8::inv(static_cast<uint8_t>(a));
+  // a^(2^w - 2): square-and-multiply over the exponent bits 1..w-1
+  uint32_t r = 1, sq = a;
+  for (int i = 1; i < w; ++i) {
+    sq = mul(sq, sq, w);
+    r = mul(r, sq, w);
+  }
+  return r;
+}
+
+bool reed_sol_vandermonde(int k, int m, int w, Mat &out) {
+  const int rows = k + m;
+  if (k < 1 || m < 1 || (w < 30 && (1 << w) < rows)) return false;
+  Mat v(static_cast<size_t>(rows) * k, 0);
+  auto at = [&](int r, int c) -> uint32_t & { return v[static_cast<size_t>(r) * k + c]; };
+  at(0, 0) = 1;
+  at(rows - 1, k - 1) = 1;
+  for (int r = 1; r < rows - 1; ++r) {
+    uint32_t p = 1;
+    for (int c = 0; c < k; ++c) { at(r, c) = p; p = mul(p, static_cast<uint32_t>(r), w); }
+  }
+  for (int piv = 1; piv < k; ++piv) {
+    int r = piv;
+    while (r < rows && at(r, piv) == 0) ++r;
+    if (r == rows) return false;
+    if (r != piv)
+      for (int c = 0; c < k; ++c) std::swap(at(r, c), at(piv, c));
+    if (at(piv, piv) != 1) {
+      const uint32_t s = inv(at(piv, piv), w);
+      for (int rr = 0; rr < rows; ++rr) at(rr, piv) = mul(s, at(rr, piv), w);
+    }
+    for (int c = 0; c < k; ++c) {
+      const uint32_t e = at(piv, c);
+      if (c == piv || e == 0) continue;
+      for (int rr = 0; rr < rows; ++rr) at(rr, c) ^= mul(e, at(rr, piv), w);
+    }
+  }
+  for (int c = 0; c < k; ++c) {
+    const uint32_t e = at(k, c);
+    if (e == 1) continue;
+    const uint32_t s = inv(e, w);
+    for (int rr = k; rr < rows; ++rr) at(rr, c) = mul(s, at(rr, c), w);
+  }
+  for (int rr = k + 1; rr < rows; ++rr) {
+    const uint32_t e = at(rr, 0);
+    if (e == 1) continue;
+    const uint32_t s = inv(e, w);
+    for (int c = 0; c < k; ++c) at(rr, c) = mul(at(rr, c), s, w);
+  }
+  out.assign(v.begin() + static_cast<size_t>(k) * k, v.end());
+  return true;
+}
+
+bool reed_sol_r6(int k, int w, Mat &out) {
+  if (k < 1) return false;
+  out.assign(2 * static_cast<size_t>(k), 1);
+  uint32_t p = 1;
+  for (int j = 0; j < k; ++j) { out[k + j] = p; p = times_x(p, w); }
+  return true;
+}
+
+int bit_block_ones(uint32_t e, int w) {
+  int n = 0;
+  for (int x = 0; x < w; ++x) { n += __builtin_popcount(e); e = times_x(e, w); }
+  return n;
+}
+
+bool cauchy_original(int k, int m, int w, Mat &out) {
+  if (k < 1 || m < 1 || (w < 31 && k + m > (1 << w))) return false;
+  out.resize(static_cast<size_t>(k) * m);
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < k; ++j) out[static_cast<size_t>(i) * k + j] = inv(static_cast<uint32_t>(i ^ (m + j)), w);
+  return true;
+}
+
+void cauchy_improve(int k, int m, int w, Mat &a) {
+  for (int j = 0; j < k; ++j) {
+    if (a[j] == 1) continue;
+    const uint32_t s = inv(a[j], w);
+    for (int i = 0; i < m; ++i) a[static_cast<size_t>(i) * k + j] = mul(a[static_cast<size_t>(i) * k + j], s, w);
+  }
+  for (int i = 1; i < m; ++i) {
+    uint32_t *row = &a[static_cast<size_t>(i) * k];
+    int best = 0, best_col = -1;
+    for (int j = 0; j < k; ++j) best += bit_block_ones(row[j], w);
+    for (int j = 0; j < k; ++j) {
+      if (row[j] == 1) continue;
+      const uint32_t s = inv(row[j], w);
+      int ones = 0;
+      for (int x = 0; x < k; ++x) ones += bit_block_ones(mul(row[x], s, w), w);
+      if (ones < best) { best = ones; best_col = j; }
+    }
+    if (best_col >= 0) {
+      const uint32_t s = inv(row[best_col], w);
+      for (int j = 0; j < k; ++j) row[j] = mul(row[j], s, w);
+    }
+  }
+}
+
+bool cauchy_good(int k, int m, int w, Mat &out) {
+  if (!cauchy_original(k, m, w, out)) return false;
+  cauchy_improve(k, m, w, out);
+  return true;
+}
+
+std::vector<int> to_bitmatrix(int k, int m, int w, const Mat &a) {
+  const int cols = k * w;
+  std::vector<int> bm(static_cast<size_t>(m) * w * cols, 0);
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < k; ++j) {
+      uint32_t e = a[static_cast<size_t>(i) * k + j];
+      for (int x = 0; x < w; ++x, e = times_x(e, w))
+        for (int l = 0; l < w; ++l) bm[static_cast<size_t>(i * w + l) * cols + j * w + x] = (e >> l) & 1;
+    }
+  return bm;
+}
+
+namespace {
+bool invert(int n, int w, Mat a, Mat &out) {
+  out.assign(static_cast<size_t>(n) * n, 0);
+  for (int i = 0; i < n; ++i) out[static_cast<size_t>(i) * n + i] = 1;
+  for (int c = 0; c < n; ++c) {
+    int p = c;
+    while (p < n && a[static_cast<size_t>(p) * n + c] == 0) ++p;
+    if (p == n) return false;
+    if (p != c)
+      for (int x = 0; x < n; ++x) {
+        std::swap(a[static_cast<size_t>(p) * n + x], a[static_cast<size_t>(c) * n + x]);
+        std::swap(out[static_cast<size_t>(p) * n + x], out[static_cast<size_t>(c) * n + x]);
+      }
+    const uint32_t s = inv(a[static_cast<size_t>(c) * n + c], w);
+    for (int x = 0; x < n; ++x) {
+      a[static_cast<size_t>(c) * n + x] = mul(a[static_cast<size_t>(c) * n + x], s, w);
+      out[static_cast<size_t>(c) * n + x] = mul(out[static_cast<size_t>(c) * n + x], s, w);
+    }
+    for (int r = 0; r < n; ++r) {
+      const uint32_t f = a[static_cast<size_t>(r) * n + c];
+      if (r == c || f == 0) continue;
+      for (int x = 0; x < n; ++x) {
+        a[static_cast<size_t>(r) * n + x] ^= mul(f, a[static_cast<size_t>(c) * n + x], w);
+        out[static_cast<size_t>(r) * n + x] ^= mul(f, out[static_cast<size_t>(c) * n + x], w);
+      }
+    }
+  }
+  return true;
+}
+}  // namespace
+
+bool make_decode(int k, int m, int w, const Mat &coding, const std::vector<int> &erased_ids, DecodePlan &dp) {
+  std::vector<char> lost(k + m, 0);
+  for (int e : erased_ids) {
+    if (e < 0 || e >= k + m) return false;
+    lost[e] = 1;
+  }
+  dp.erased.clear();
+  dp.survivors.clear();
+  for (int i = 0; i < k + m; ++i) {
+    if (lost[i]) dp.erased.push_back(i);
+    else if (static_cast<int>(dp.survivors.size()) < k) dp.survivors.push_back(i);
+  }
+  if (static_cast<int>(dp.survivors.size()) < k) return false;
+  Mat s(static_cast<size_t>(k) * k, 0), sinv;
+  for (int j = 0; j < k; ++j) {
+    const int id = dp.survivors[j];
+    if (id < k) s[static_cast<size_t>(j) * k + id] = 1;
+    else std::copy_n(&coding[static_cast<size_t>(id - k) * k], k, &s[static_cast<size_t>(j) * k]);
+  }
+  if (!invert(k, w, s, sinv)) return false;
+  dp.rows.assign(dp.erased.size() * k, 0);
+  for (size_t r = 0; r < dp.erased.size(); ++r) {
+    const int id = dp.erased[r];
+    uint32_t *dst = &dp.rows[r * k];
+    if (id < k) {
+      std::copy_n(&sinv[static_cast<size_t>(id) * k], k, dst);
+    } else {
+      const uint32_t *crow = &coding[static_cast<size_t>(id - k) * k];
+      for (int j = 0; j < k; ++j) {
+        uint32_t acc = 0;
+        for (int t = 0; t < k; ++t) acc ^= mul(crow[t], sinv[static_cast<size_t>(t) * k + j], w);
+        dst[j] = acc;
+      }
+    }
+  }
+  return true;
+}
+
+}  // namespace gfw
 }  // namespace lsec

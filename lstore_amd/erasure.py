@@ -172,9 +172,9 @@ class Plan:
         return cls(lib().et_new_plan(method, strip_size, k, m, w, packet_size, base_unit))
 
     @classmethod
-    def for_chunk(cls, method, k, m, chunk) -> "Plan":
+    def for_chunk(cls, method, k, m, chunk, w=-1) -> "Plan":
         """The plan segment/jerasure.c:2236-2243 builds: et_generate_plan(k*C, ...) + form_*."""
-        p = cls.generate(k * chunk, method, k, m)
+        p = cls.generate(k * chunk, method, k, m, w)
         p.form_encoding_matrix()
         p.form_decoding_matrix()
         return p
@@ -215,7 +215,8 @@ class Plan:
 
     @property
     def kernel(self) -> int:
-        """1 = bytewise (matrix codes), 2 = bitsliced (Cauchy), 0 = no GPU kernel"""
+        """1 = bytewise GF(2^8), 2 = bitsliced GF(2^8) (Cauchy), 3 = GF(2) bitmatrix (liberation
+        family, Cauchy at w = 16/32), 4 = wordwise GF(2^16/2^32) (RS), 0 = no GPU kernel"""
         return lib().lsec_plan_kernel(self._p)
 
     def matrix(self):

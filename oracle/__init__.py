@@ -131,7 +131,7 @@ def encode(method, data, m, packet=0, w=8):
             raise ValueError("bitmatrix encode: size must be a multiple of w*packet")
     else:
         mat = np.ascontiguousarray(mat)
-        lib.eco_matrix_encode(k, m, mat.ctypes.data_as(C.c_void_p), d, p, size)
+        lib.eco_matrix_encode(k, m, w, mat.ctypes.data_as(C.c_void_p), d, p, size)
     return par
 
 
@@ -147,7 +147,7 @@ def decode(method, shards, k, erasures, packet=0, w=8):
         bm = np.ascontiguousarray(bitmatrix(mat, w))
         return lib.eco_bitmatrix_decode(k, m, w, bm.ctypes.data_as(C.c_void_p), er, ptrs, size, packet)
     mat = np.ascontiguousarray(mat)
-    return lib.eco_matrix_decode(k, m, mat.ctypes.data_as(C.c_void_p), er, ptrs, size)
+    return lib.eco_matrix_decode(k, m, w, mat.ctypes.data_as(C.c_void_p), er, ptrs, size)
 
 
 def adler32(buf, adler=1):

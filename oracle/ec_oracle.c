@@ -13,10 +13,10 @@
  * generator tests/golden/make_golden.py) and against the known-answer anchors
  * recorded in SURVEY.md §8c.
  *
- * Scope: w = 8 (the only word size on the BASELINE configs), all matrix
- * methods (reed_sol_van, reed_sol_r6_op, cauchy_orig, cauchy_good, raid4) and
- * generic bitmatrix encode/decode (any w) for the bitmatrix methods.
- * Clarity over speed: plain byte loops.
+ * Scope: w = 8, 16 and 32 (what erasure_tools.c:806-811 accepts) for all
+ * matrix methods (reed_sol_van, reed_sol_r6_op, cauchy_orig, cauchy_good,
+ * raid4), and generic bitmatrix encode/decode (any w) for the bitmatrix
+ * methods.  Clarity over speed: plain element loops.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -58,22 +58,55 @@ int eco_div(int a, int b)
     return g_exp[g_log[a] + 255 - g_log[b]];
 }
 
+/* GF(2^w) for w = 16 and 32: shift-and-add multiply modulo Jerasure's primitive
+ * polynomials (galois.c:65-98: prim_poly[16] = 0210013, prim_poly[32] = 020000007
+ * with the x^32 term implied), as galois_shift_multiply (galois.c:343-371) does.
+ * Multiplication in a field is unique, so this equals the log tables (w = 16,
+ * galois.c:169-213) and the split-w8 tables (w = 32, galois.c:817-880). */
+static uint32_t poly_w(int w) { return w == 16 ? 0x1100Bu : w == 32 ? 0x00400007u : 0x11Du; }
+
+uint32_t eco_mulw(uint32_t a, uint32_t b, int w)
+{
+    if (w == 8) return (uint32_t)eco_mul((int)a, (int)b);
+    uint32_t prod = 0, top = 1u << (w - 1), mask = w == 32 ? 0xFFFFFFFFu : (1u << w) - 1;
+    for (int i = 0; i < w; i++) {
+        if (a & (1u << i)) prod ^= b;
+        b = (b & top) ? ((b << 1) ^ poly_w(w)) & mask : (b << 1) & mask;
+    }
+    return prod;
+}
+
+/* a^(2^w - 2) = a^-1 (any correct inverse equals galois_shift_inverse / the log tables) */
+uint32_t eco_invw(uint32_t a, int w)
+{
+    if (w == 8) return (uint32_t)eco_div(1, (int)a);
+    uint32_t r = 1, base = a;
+    for (int i = 1; i < w; i++) {      /* exponent bits 1..w-1 are set, bit 0 is clear */
+        base = eco_mulw(base, base, w);
+        r = eco_mulw(r, base, w);
+    }
+    return r;
+}
+
+
 /* ---------------- coding matrices ---------------------------------------- */
+/* Matrices are int arrays as in Jerasure; for w = 32 an element is the int's bit pattern. */
+#define U(x) ((uint32_t)(x))
 
 /* reed_sol_vandermonde_coding_matrix (reed_sol.c:79-99) via the systematic
  * distribution matrix (reed_sol.c:242-367): column-reduce an extended
  * Vandermonde matrix to [I;C], normalise row k to ones, then every later row's
  * first column to one. */
-static int rs_vandermonde(int k, int m, int *out)
+static int rs_vandermonde(int k, int m, int w, int *out)
 {
     int rows = k + m, cols = k;
-    if (rows > 256 || cols >= rows) return -1;
-    int *d = (int *)calloc((size_t)rows * cols, sizeof(int));
+    if ((w < 30 && (1 << w) < rows) || cols >= rows) return -1;   /* reed_sol.c:247-248 */
+    uint32_t *d = (uint32_t *)calloc((size_t)rows * cols, sizeof(uint32_t));
     d[0] = 1;                                  /* row 0 = e_0          */
     d[(rows - 1) * cols + cols - 1] = 1;       /* last row = e_{k-1}   */
     for (int i = 1; i < rows - 1; i++) {       /* row i = (1, i, i^2, ...) */
-        int v = 1;
-        for (int j = 0; j < cols; j++) { d[i * cols + j] = v; v = eco_mul(v, i); }
+        uint32_t v = 1;
+        for (int j = 0; j < cols; j++) { d[i * cols + j] = v; v = eco_mulw(v, U(i), w); }
     }
     for (int i = 1; i < cols; i++) {
         int r = i;
@@ -81,76 +114,77 @@ static int rs_vandermonde(int k, int m, int *out)
         if (r >= rows) { free(d); return -1; }
         if (r != i)
             for (int c = 0; c < cols; c++) {
-                int t = d[r * cols + c]; d[r * cols + c] = d[i * cols + c]; d[i * cols + c] = t;
+                uint32_t t = d[r * cols + c]; d[r * cols + c] = d[i * cols + c]; d[i * cols + c] = t;
             }
         if (d[i * cols + i] != 1) {
-            int inv = eco_div(1, d[i * cols + i]);
-            for (int rr = 0; rr < rows; rr++) d[rr * cols + i] = eco_mul(inv, d[rr * cols + i]);
+            uint32_t inv = eco_invw(d[i * cols + i], w);
+            for (int rr = 0; rr < rows; rr++) d[rr * cols + i] = eco_mulw(inv, d[rr * cols + i], w);
         }
         for (int j = 0; j < cols; j++) {
-            int e = d[i * cols + j];
+            uint32_t e = d[i * cols + j];
             if (j == i || e == 0) continue;
-            for (int rr = 0; rr < rows; rr++) d[rr * cols + j] ^= eco_mul(e, d[rr * cols + i]);
+            for (int rr = 0; rr < rows; rr++) d[rr * cols + j] ^= eco_mulw(e, d[rr * cols + i], w);
         }
     }
     for (int j = 0; j < cols; j++) {           /* row k -> all ones */
-        int e = d[cols * cols + j];
+        uint32_t e = d[cols * cols + j];
         if (e == 1) continue;
-        int inv = eco_div(1, e);
-        for (int rr = cols; rr < rows; rr++) d[rr * cols + j] = eco_mul(inv, d[rr * cols + j]);
+        uint32_t inv = eco_invw(e, w);
+        for (int rr = cols; rr < rows; rr++) d[rr * cols + j] = eco_mulw(inv, d[rr * cols + j], w);
     }
     for (int rr = cols + 1; rr < rows; rr++) { /* column 0 -> all ones */
-        int e = d[rr * cols];
+        uint32_t e = d[rr * cols];
         if (e == 1) continue;
-        int inv = eco_div(1, e);
-        for (int j = 0; j < cols; j++) d[rr * cols + j] = eco_mul(d[rr * cols + j], inv);
+        uint32_t inv = eco_invw(e, w);
+        for (int j = 0; j < cols; j++) d[rr * cols + j] = eco_mulw(d[rr * cols + j], inv, w);
     }
-    memcpy(out, d + cols * cols, sizeof(int) * m * k);
+    for (int i = 0; i < m * k; i++) out[i] = (int)d[cols * cols + i];
     free(d);
     return 0;
 }
 
 /* number of ones in the w x w bit-block of n (what cauchy_n_ones, cauchy.c:92-132, counts) */
-static int n_ones8(int n)
+static int n_ones(uint32_t n, int w)
 {
     int total = 0;
-    for (int x = 0; x < 8; x++) {
-        total += __builtin_popcount((unsigned)n);
-        n = eco_mul(n, 2);
+    for (int x = 0; x < w; x++) {
+        total += __builtin_popcount(n);
+        n = eco_mulw(n, 2, w);
     }
     return total;
 }
 
 /* cauchy_original_coding_matrix (cauchy.c:134-150): M[i][j] = 1/(i xor (m+j)) */
-static int cauchy_orig(int k, int m, int *out)
+static int cauchy_orig(int k, int m, int w, int *out)
 {
-    if (k + m > 256) return -1;
+    if (w < 31 && k + m > (1 << w)) return -1;
     for (int i = 0; i < m; i++)
-        for (int j = 0; j < k; j++) out[i * k + j] = eco_div(1, i ^ (m + j));
+        for (int j = 0; j < k; j++) out[i * k + j] = (int)eco_invw(U(i ^ (m + j)), w);
     return 0;
 }
 
 /* cauchy_improve_coding_matrix (cauchy.c:169-210) */
-static void cauchy_improve(int k, int m, int *M)
+static void cauchy_improve(int k, int m, int w, int *M)
 {
     for (int j = 0; j < k; j++) {
         if (M[j] == 1) continue;
-        int inv = eco_div(1, M[j]);
-        for (int i = 0; i < m; i++) M[i * k + j] = eco_mul(M[i * k + j], inv);
+        uint32_t inv = eco_invw(U(M[j]), w);
+        for (int i = 0; i < m; i++) M[i * k + j] = (int)eco_mulw(U(M[i * k + j]), inv, w);
     }
     for (int i = 1; i < m; i++) {
         int *row = M + i * k;
         int best = 0, best_j = -1;
-        for (int j = 0; j < k; j++) best += n_ones8(row[j]);
+        for (int j = 0; j < k; j++) best += n_ones(U(row[j]), w);
         for (int j = 0; j < k; j++) {
             if (row[j] == 1) continue;
-            int inv = eco_div(1, row[j]), tot = 0;
-            for (int x = 0; x < k; x++) tot += n_ones8(eco_mul(row[x], inv));
+            uint32_t inv = eco_invw(U(row[j]), w);
+            int tot = 0;
+            for (int x = 0; x < k; x++) tot += n_ones(eco_mulw(U(row[x]), inv, w), w);
             if (tot < best) { best = tot; best_j = j; }
         }
         if (best_j >= 0) {
-            int inv = eco_div(1, row[best_j]);
-            for (int j = 0; j < k; j++) row[j] = eco_mul(row[j], inv);
+            uint32_t inv = eco_invw(U(row[best_j]), w);
+            for (int j = 0; j < k; j++) row[j] = (int)eco_mulw(U(row[j]), inv, w);
         }
     }
 }
@@ -170,32 +204,33 @@ static const uint8_t CBEST8[255] = {
     99, 105, 114, 121, 124, 178, 209, 213, 223, 228, 241, 254, 60, 191, 198, 247, 120, 240, 107, 127,
     144, 145, 177, 211, 214, 246, 245, 123, 126, 187, 231, 253, 63, 179, 229, 244, 61, 122, 215, 252};
 
-/* cauchy_good_general_coding_matrix (cauchy.c:212-241) */
-static int cauchy_good(int k, int m, int *out)
+/* cauchy_good_general_coding_matrix (cauchy.c:212-241); cbest tables exist for
+ * w <= 11 only (cbest_max_k, cauchy.c:81-83), so w = 16/32 always improves. */
+static int cauchy_good(int k, int m, int w, int *out)
 {
-    if (m == 2 && k <= 255) {
+    if (w == 8 && m == 2 && k <= 255) {
         for (int j = 0; j < k; j++) { out[j] = 1; out[k + j] = CBEST8[j]; }
         return 0;
     }
-    if (cauchy_orig(k, m, out)) return -1;
-    cauchy_improve(k, m, out);
+    if (cauchy_orig(k, m, w, out)) return -1;
+    cauchy_improve(k, m, w, out);
     return 0;
 }
 
 int eco_coding_matrix(int method, int k, int m, int w, int *out)
 {
     eco_init();
-    if (w != 8) return -1;
+    if (w != 8 && w != 16 && w != 32) return -1;
     switch (method) {
-    case ECO_REED_SOL_VAN: return rs_vandermonde(k, m, out);
+    case ECO_REED_SOL_VAN: return rs_vandermonde(k, m, w, out);
     case ECO_REED_SOL_R6_OP: {             /* reed_sol_r6_coding_matrix, reed_sol.c:59-77 */
         if (m != 2) return -1;
-        int v = 1;
-        for (int j = 0; j < k; j++) { out[j] = 1; out[k + j] = v; v = eco_mul(v, 2); }
+        uint32_t v = 1;
+        for (int j = 0; j < k; j++) { out[j] = 1; out[k + j] = (int)v; v = eco_mulw(v, 2, w); }
         return 0;
     }
-    case ECO_CAUCHY_ORIG: return cauchy_orig(k, m, out);
-    case ECO_CAUCHY_GOOD: return cauchy_good(k, m, out);
+    case ECO_CAUCHY_ORIG: return cauchy_orig(k, m, w, out);
+    case ECO_CAUCHY_GOOD: return cauchy_good(k, m, w, out);
     case ECO_RAID4:
         if (m != 1) return -1;
         for (int j = 0; j < k; j++) out[j] = 1;
@@ -209,14 +244,14 @@ int eco_coding_matrix(int method, int k, int m, int w, int *out)
 int eco_matrix_to_bitmatrix(int k, int m, int w, const int *M, int *out)
 {
     eco_init();
-    if (w != 8) return -1;
+    if (w != 8 && w != 16 && w != 32) return -1;
     int cols = k * w;
     for (int i = 0; i < m; i++)
         for (int j = 0; j < k; j++) {
-            int e = M[i * k + j];
+            uint32_t e = U(M[i * k + j]);
             for (int x = 0; x < w; x++) {
                 for (int l = 0; l < w; l++) out[(i * w + l) * cols + j * w + x] = (e >> l) & 1;
-                e = eco_mul(e, 2);
+                e = eco_mulw(e, 2, w);
             }
         }
     return 0;
@@ -291,22 +326,33 @@ int eco_generate_plan(long long file_size, int method, int k, int m, int w, int 
 
 /* ---------------- encode ------------------------------------------------- */
 
-/* jerasure_matrix_encode semantics (jerasure.c:301-315, :579-639), w = 8:
- * coding[i][b] = XOR_j M[i][j] * data[j][b] */
-void eco_matrix_encode(int k, int m, const int *M, char **data, char **coding, int size)
+/* jerasure_matrix_encode semantics (jerasure.c:301-315, :579-639):
+ * coding[i][t] = XOR_j M[i][j] * data[j][t] over elements t of w bits, stored as
+ * native little-endian bytes / uint16 / uint32 (galois_w{08,16,32}_region_multiply,
+ * galois.c:471-525, :527-604, :730-810).  size is in bytes. */
+void eco_matrix_encode(int k, int m, int w, const int *M, char **data, char **coding, int size)
 {
     eco_init();
+    int n = size / (w / 8);
     for (int i = 0; i < m; i++) {
-        uint8_t *o = (uint8_t *)coding[i];
-        memset(o, 0, size);
+        memset(coding[i], 0, size);
         for (int j = 0; j < k; j++) {
-            int c = M[i * k + j];
-            const uint8_t *s = (const uint8_t *)data[j];
+            uint32_t c = U(M[i * k + j]);
             if (c == 0) continue;
-            if (c == 1) { for (int b = 0; b < size; b++) o[b] ^= s[b]; continue; }
-            uint8_t tab[256];
-            for (int v = 0; v < 256; v++) tab[v] = (uint8_t)eco_mul(c, v);
-            for (int b = 0; b < size; b++) o[b] ^= tab[s[b]];
+            if (w == 8) {
+                uint8_t *o = (uint8_t *)coding[i], tab[256];
+                const uint8_t *src = (const uint8_t *)data[j];
+                for (int v = 0; v < 256; v++) tab[v] = (uint8_t)eco_mul((int)c, v);
+                for (int t = 0; t < n; t++) o[t] ^= tab[src[t]];
+            } else if (w == 16) {
+                uint16_t *o = (uint16_t *)coding[i];
+                const uint16_t *src = (const uint16_t *)data[j];
+                for (int t = 0; t < n; t++) o[t] ^= (uint16_t)eco_mulw(c, src[t], 16);
+            } else {
+                uint32_t *o = (uint32_t *)coding[i];
+                const uint32_t *src = (const uint32_t *)data[j];
+                for (int t = 0; t < n; t++) o[t] ^= eco_mulw(c, src[t], 32);
+            }
         }
     }
 }
@@ -348,8 +394,8 @@ static int to_erased(int k, int m, const int *erasures, int *erased)
     return 0;
 }
 
-/* Gauss-Jordan inverse over GF(2^8); returns -1 if singular */
-static int gf_invert(int n, int *a, int *inv)
+/* Gauss-Jordan inverse over GF(2^w); returns -1 if singular */
+static int gf_invert(int n, int w, uint32_t *a, uint32_t *inv)
 {
     for (int i = 0; i < n * n; i++) inv[i] = 0;
     for (int i = 0; i < n; i++) inv[i * n + i] = 1;
@@ -359,15 +405,15 @@ static int gf_invert(int n, int *a, int *inv)
         if (p == n) return -1;
         if (p != c)
             for (int x = 0; x < n; x++) {
-                int t = a[p * n + x]; a[p * n + x] = a[c * n + x]; a[c * n + x] = t;
+                uint32_t t = a[p * n + x]; a[p * n + x] = a[c * n + x]; a[c * n + x] = t;
                 t = inv[p * n + x]; inv[p * n + x] = inv[c * n + x]; inv[c * n + x] = t;
             }
-        int s = eco_div(1, a[c * n + c]);
-        for (int x = 0; x < n; x++) { a[c * n + x] = eco_mul(a[c * n + x], s); inv[c * n + x] = eco_mul(inv[c * n + x], s); }
+        uint32_t s = eco_invw(a[c * n + c], w);
+        for (int x = 0; x < n; x++) { a[c * n + x] = eco_mulw(a[c * n + x], s, w); inv[c * n + x] = eco_mulw(inv[c * n + x], s, w); }
         for (int r = 0; r < n; r++) {
-            int f = a[r * n + c];
+            uint32_t f = a[r * n + c];
             if (r == c || f == 0) continue;
-            for (int x = 0; x < n; x++) { a[r * n + x] ^= eco_mul(f, a[c * n + x]); inv[r * n + x] ^= eco_mul(f, inv[c * n + x]); }
+            for (int x = 0; x < n; x++) { a[r * n + x] ^= eco_mulw(f, a[c * n + x], w); inv[r * n + x] ^= eco_mulw(f, inv[c * n + x], w); }
         }
     }
     return 0;
@@ -376,28 +422,30 @@ static int gf_invert(int n, int *a, int *inv)
 /* Recover erased devices from the first k survivors (the choice made by
  * jerasure_make_decoding_matrix, jerasure.c:100-128).  Because the code is MDS
  * the recovered bytes are unique, so any correct decode equals jerasure's. */
-int eco_matrix_decode(int k, int m, const int *M, const int *erasures, char **ptrs, int size)
+int eco_matrix_decode(int k, int m, int w, const int *M, const int *erasures, char **ptrs, int size)
 {
     eco_init();
     int erased[512], ids[256];
     if (k + m > 512 || to_erased(k, m, erasures, erased)) return -1;
     int n = 0;
     for (int i = 0; n < k; i++) if (!erased[i]) ids[n++] = i;
-    int *a = (int *)malloc(sizeof(int) * k * k), *inv = (int *)malloc(sizeof(int) * k * k);
+    uint32_t *a = (uint32_t *)malloc(sizeof(uint32_t) * k * k), *inv = (uint32_t *)malloc(sizeof(uint32_t) * k * k);
+    int *row = (int *)malloc(sizeof(int) * k);
     for (int r = 0; r < k; r++)
         for (int c = 0; c < k; c++)
-            a[r * k + c] = ids[r] < k ? (ids[r] == c) : M[(ids[r] - k) * k + c];
-    if (gf_invert(k, a, inv)) { free(a); free(inv); return -1; }
+            a[r * k + c] = ids[r] < k ? (uint32_t)(ids[r] == c) : U(M[(ids[r] - k) * k + c]);
+    if (gf_invert(k, w, a, inv)) { free(a); free(inv); free(row); return -1; }
     char **surv = (char **)malloc(sizeof(char *) * k);
     for (int j = 0; j < k; j++) surv[j] = ptrs[ids[j]];
     for (int i = 0; i < k; i++) {
         if (!erased[i]) continue;
         char *out = ptrs[i];
-        eco_matrix_encode(k, 1, inv + i * k, surv, &out, size);
+        for (int j = 0; j < k; j++) row[j] = (int)inv[i * k + j];
+        eco_matrix_encode(k, 1, w, row, surv, &out, size);
     }
     for (int i = 0; i < m; i++)
-        if (erased[k + i]) eco_matrix_encode(k, 1, M + i * k, ptrs, &ptrs[k + i], size);
-    free(surv); free(a); free(inv);
+        if (erased[k + i]) eco_matrix_encode(k, 1, w, M + i * k, ptrs, &ptrs[k + i], size);
+    free(surv); free(a); free(inv); free(row);
     return 0;
 }
 

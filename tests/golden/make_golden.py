@@ -44,6 +44,11 @@ def plan_entries():
             (O.CAUCHY_GOOD, 2, 2, 8), (O.CAUCHY_GOOD, 32, 2, 8), (O.CAUCHY_GOOD, 3, 5, 8),
             (O.REED_SOL_VAN, 3, 5, 8), (O.REED_SOL_VAN, 32, 8, 8),
             (O.LIBERATION, 6, 2, 7), (O.BLAUM_ROTH, 6, 2, 6), (O.LIBER8TION, 6, 2, 8)]
+    # wide fields (erasure_tools.c:806-811 accepts w = 16 / 32 for the matrix methods)
+    for w in (16, 32):
+        out += [(O.REED_SOL_VAN, 6, 3, w), (O.REED_SOL_VAN, 10, 4, w), (O.REED_SOL_R6_OP, 6, 2, w),
+                (O.CAUCHY_ORIG, 6, 3, w), (O.CAUCHY_GOOD, 6, 3, w), (O.CAUCHY_GOOD, 10, 4, w),
+                (O.CAUCHY_GOOD, 4, 2, w)]
     return out
 
 
@@ -93,6 +98,13 @@ def cases():
     # bitmatrix families (not on the configs; fixtures for the next row)
     c += [(O.LIBERATION, 6, 2, 7, 7 * 64 * 4, 64, "splitmix"), (O.BLAUM_ROTH, 6, 2, 6, 6 * 64 * 4, 64, "splitmix"),
           (O.LIBER8TION, 6, 2, 8, 8 * 64 * 4, 64, "splitmix")]
+    # wide fields: little-endian uint16 / uint32 elements (matrix codes), w*P super-packets (Cauchy)
+    for w in (16, 32):
+        for pat in ("affine", "splitmix"):
+            c += [(O.REED_SOL_VAN, 6, 3, w, 1024, 0, pat), (O.CAUCHY_GOOD, 6, 3, w, 1024, 1024 // w, pat)]
+        c += [(O.REED_SOL_VAN, 10, 4, w, 4096, 0, "splitmix"), (O.REED_SOL_R6_OP, 6, 2, w, 1024, 0, "splitmix"),
+              (O.CAUCHY_ORIG, 6, 3, w, 2048, 2048 // w, "splitmix"), (O.CAUCHY_GOOD, 10, 4, w, 4096, 64, "splitmix"),
+              (O.REED_SOL_VAN, 6, 3, w, 65536, 0, "splitmix")]
     return c
 
 

@@ -77,6 +77,55 @@ def test_liberation_family_vs_reference(cuda, method, k, w):
             assert np.array_equal(sh, full), er
 
 
+# ---------------------------------------------------------------- wide fields (w = 16 / 32)
+@pytest.mark.parametrize("method,k,m,w,size,P", [
+    (L.REED_SOL_VAN, 6, 3, 16, 4104, 0),      # 4104 % 16 == 8: ragged last lane
+    (L.REED_SOL_VAN, 10, 4, 32, 8200, 0),
+    (L.REED_SOL_VAN, 20, 6, 16, 65536, 0),
+    (L.REED_SOL_VAN, 12, 9, 32, 4096, 0),     # R = 9 > 8: two launches
+    (L.REED_SOL_R6_OP, 6, 2, 16, 2056, 0),
+    (L.REED_SOL_R6_OP, 9, 2, 32, 4096, 0),
+    (L.CAUCHY_GOOD, 6, 3, 16, 16 * 64 * 3, 64),
+    (L.CAUCHY_ORIG, 5, 4, 16, 16 * 32 * 2, 32),
+    (L.CAUCHY_GOOD, 10, 4, 32, 32 * 32 * 4, 32),
+])
+def test_wide_fields_vs_oracle(cuda, method, k, m, w, size, P):
+    """RS / r6 over GF(2^16) / GF(2^32) (wordwise kernel, little-endian words) and Cauchy at
+    w = 16 / 32 (GF(2) bitmatrix kernel): encode and every single + some double/triple
+    erasure decodes, bit-exact vs the oracle restatement (pinned to the reference fixtures)."""
+    import torch
+
+    n = 3
+    st = np.zeros((n, k + m, size), dtype=np.uint8)
+    st[:, :k] = np.random.default_rng(k * w + m).integers(0, 256, (n, k, size), dtype=np.uint8)
+    st[0, 0] = 0xFF
+    with L.Plan.new(method, size, k, m, w, P, 8) as p:
+        assert p.form_encoding_matrix() == 0 and p.form_decoding_matrix() == 0
+        p.encode_stripes(st)
+        for s in range(n):
+            assert np.array_equal(st[s, k:], O.encode(method, st[s, :k], m, P, w)), s
+        if O.ref_available():
+            rp = O.RefPlan(method, k, m, w, P)
+            assert np.array_equal(rp.encode(st[1, :k].copy()), st[1, k:])
+            rp.close()
+        full = st.copy()
+        pats = [[e] for e in range(k + m)] + [[0, k], [k - 1, k + m - 1]]
+        if m >= 3:
+            pats.append([1, 2, k + 1])
+        for pat in pats:
+            st[:, pat] = 0x3C
+            p.decode_stripes(st, pat)
+            assert np.array_equal(st, full), pat
+        d = torch.from_numpy(full[:, :k].copy()).to(cuda)
+        par = torch.zeros((n, m, size), dtype=torch.uint8, device=cuda)
+        p.encode_dev(d, par)
+        out = torch.zeros((n, 2, size), dtype=torch.uint8, device=cuda)
+        p.decode_dev(d, par, [0, k], out=out)
+        torch.cuda.synchronize()
+        assert np.array_equal(par.cpu().numpy(), full[:, k:])
+        assert np.array_equal(out.cpu().numpy(), full[:, [0, k]])
+
+
 # ---------------------------------------------------------------- encode, device-resident
 def test_encode_dev_matches_reference(cuda, golden):
     import torch

@@ -173,10 +173,15 @@ def test_no_gpu_means_loud_failure(built):
 
 
 def test_unsupported_method_is_an_error_not_a_fallback(built):
-    with L.Plan.new(L.REED_SOL_VAN, 0, 6, 3, 16, 8, 8) as p:   # w = 16: no GPU kernel in this build
+    with L.Plan.new(L.LIBERATION, 0, 6, 2, 37, 8, 8) as p:   # a prime w outside the instantiated list
         assert p.kernel == 0
-        st = np.zeros((1, 9, 4096), np.uint8)
+        st = np.zeros((1, 8, 37 * 8 * 4), np.uint8)
         with pytest.raises(E.ErasureError, match="no GPU kernel"):
             p.encode_stripes(st)
+    for w in (16, 32):
+        with L.Plan.new(L.REED_SOL_VAN, 0, 6, 3, w, 8, 8) as p:
+            assert p.kernel == 4   # wordwise GF(2^w)
+        with L.Plan.new(L.CAUCHY_GOOD, 0, 6, 3, w, 8, 8) as p:
+            assert p.kernel == 3   # generic bitmatrix
     with L.Plan.generate(6 * 7 * 64 * 4, L.LIBERATION, 6, 2) as p:
         assert p.kernel == 3   # generic bitmatrix kernel

@@ -26,6 +26,11 @@ CONFIGS = {
     "rs124": (L.REED_SOL_VAN, 12, 4, 1 << 20),
     "rs84": (L.REED_SOL_VAN, 8, 4, 1 << 20),
     "cg206": (L.CAUCHY_GOOD, 20, 6, 256 << 10),
+    # wide fields (w = 16 / 32): wordwise RS, bitmatrix Cauchy
+    "rs63w16": (L.REED_SOL_VAN, 6, 3, 1 << 20, 16),
+    "rs63w32": (L.REED_SOL_VAN, 6, 3, 1 << 20, 32),
+    "cg63w16": (L.CAUCHY_GOOD, 6, 3, 1 << 20, 16),
+    "cg63w32": (L.CAUCHY_GOOD, 6, 3, 1 << 20, 32),
 }
 
 
@@ -36,13 +41,15 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--configs", default="rs63,cg104,cg63")
     ap.add_argument("--variants", default="0,0;1,0;0,2;0,4")
+    ap.add_argument("--magic", action="store_true", help="also time fused encode+magic and standalone magic")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     variants = [tuple(int(x) for x in v.split(",")) for v in a.variants.split(";")]
     for name in a.configs.split(","):
-        meth, k, m, C = CONFIGS[name]
+        meth, k, m, C = CONFIGS[name][:4]
+        w = CONFIGS[name][4] if len(CONFIGS[name]) > 4 else -1
         N = max(8, int(a.data_gib * 2**30 / (k * C)))
-        plan = L.Plan.for_chunk(meth, k, m, C)
+        plan = L.Plan.for_chunk(meth, k, m, C, w)
         data = torch.randint(0, 256, (N, k, C), dtype=torch.uint8, device=dev)
         par = torch.empty((N, m, C), dtype=torch.uint8, device=dev)
         out = torch.empty((N, 1, C), dtype=torch.uint8, device=dev)
@@ -76,6 +83,22 @@ def main():
                   f"({eb / te / 8e9:5.1%})   decode {td:8.3f} ms {db / td / 1e6:7.1f} GB/s ({db / td / 8e9:5.1%})",
                   flush=True)
         E.set_kernel_variant(0, 0)
+        if a.magic:
+            mg = torch.zeros((N, 4), dtype=torch.uint8, device=dev)
+            tm = []
+            for fn in (lambda: plan.encode_magic_dev(data, par, mg), lambda: plan.stripe_magic_dev(data, par, mg)):
+                fn()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(a.reps):
+                    fn()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                tm.append(e0.elapsed_time(e1) / a.reps)
+            eb = (k + m) * C * N
+            print(f"{name:6s} encode+magic fused {tm[0]:8.3f} ms {eb / tm[0] / 1e6:7.1f} GB/s ({eb / tm[0] / 8e9:5.1%})   "
+                  f"magic alone {tm[1]:8.3f} ms {eb / tm[1] / 1e6:7.1f} GB/s ({eb / tm[1] / 8e9:5.1%})", flush=True)
+            del mg
         del data, par, out, ref_par
         plan.close()
         torch.cuda.empty_cache()
