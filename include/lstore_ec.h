@@ -140,17 +140,55 @@ int lsec_stripe_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, 
 int lsec_segment_write(lio_erasure_plan_t *plan, const char *data, int nstripes, int chunk, int n_shift,
                        long long first_stripe, char **dev);
 
+/* Flags of the read / inspect entry points */
+#define LSEC_READ_PARANOID 1   /* verify every stripe, not only those with bad chunks */
+#define LSEC_MAGIC_LEGACY  2   /* segment magic_cksum == 0: magics are not adler32 sums, so
+                                  stripes are verified with control chunks (jerasure.c:218-266) */
+#define LSEC_INSPECT_FIX   4   /* inspect: repair in place (INSPECT_{QUICK,SCAN,FULL}_REPAIR) */
+#define LSEC_MAX_DEVS      64
+
 /* Batched read side for whole stripes (segjerase_read_func, segment/jerasure.c:1255-1631):
  * dev[i] are device images laid out as lsec_segment_write writes them (NULL = device
  * unreadable).  Per stripe: majority vote over the stored magics (:1383-1438); stripes with
- * chunks outside the quorum are rebuilt (decode) and verified against the quorum magic
- * (jerase_control_check, :202-269), falling back to the brute-force search over erasure
- * combinations of 1..m devices (jerase_brute_recovery, :321-339); with `paranoid` every
- * stripe is verified.  Checks and rebuilds run as GPU batches.  User data (nstripes*k*C)
- * goes to data_out; status[s] (optional) = 0 ok, 1 recovered, 2 blank (zero-filled),
- * -1 unrecoverable.  Returns the number of unrecoverable stripes, or -1 on error. */
+ * chunks outside the quorum are rebuilt (decode) and verified (jerase_control_check,
+ * :202-269: against the quorum magic, or with control chunks under LSEC_MAGIC_LEGACY),
+ * falling back to the brute-force search over erasure combinations (jerase_brute_recovery,
+ * :321-339); with LSEC_READ_PARANOID every stripe is verified.  Checks and rebuilds run as
+ * GPU batches.  User data (nstripes*k*C) goes to data_out; status[s] (optional) = 0 ok,
+ * 1 recovered (a data chunk was rebuilt), 2 blank (zero-filled), -1 unrecoverable.  Returns the number of
+ * unrecoverable stripes, or -1 on error. */
 int lsec_segment_read(lio_erasure_plan_t *plan, char **dev, int nstripes, int chunk, int n_shift,
-                      long long first_stripe, int paranoid, char *data_out, int *status);
+                      long long first_stripe, int flags, char *data_out, int *status);
+
+/* Full byte-level inspection and optional repair (segjerase_inspect_full_func,
+ * segment/jerasure.c:347-732).  buf holds nstripes stripes as the inspection reads them from
+ * the LUN child: stripe-major, k+m records of [4-byte magic | chunk] each
+ * (stripe_size_with_magic = (k+m)*(C+4)).  Every stripe is classified as the reference does:
+ * stripe_status[s] = LSEC_STRIPE_*; badmap[s*(k+m)+j] = 1 for the devices the reference's
+ * badmap holds after the stripe (what [DEVMAP] prints).  With LSEC_INSPECT_FIX the repaired
+ * chunks and magics are written into buf and rewrite[s*(k+m)+j] = 1 marks every record the
+ * reference writes back (all of them under LSEC_MAGIC_LEGACY, which converts the stripe to
+ * adler32 magics).  `state` carries the counters and the brute-force guess between
+ * consecutive calls of one inspection (zero it first).  Returns 0, or -1 on error. */
+enum {
+  LSEC_STRIPE_OK = 0,            /* every magic agrees and the stripe verifies */
+  LSEC_STRIPE_EMPTY = 1,         /* never written: zero magics, zero data (skipped) */
+  LSEC_STRIPE_BAD_MAGIC = 2,     /* some magics disagree; the rebuild of those devices verifies */
+  LSEC_STRIPE_REPAIRED = 3,      /* silent corruption found by the brute-force search ("r-mismatch") */
+  LSEC_STRIPE_LOST_MAGIC = 4,    /* too few matching magics to rebuild ("magic") */
+  LSEC_STRIPE_LOST_MISMATCH = 5  /* data and parity disagree beyond repair ("u-mismatch") */
+};
+typedef struct {
+  long long bad_stripes;      /* sf->bad_stripes (bad_count) */
+  long long unrecoverable;    /* unrecoverable_count */
+  long long silent_errors;    /* erasure_errors: stripes whose check failed */
+  long long empty_stripes;    /* n_empty */
+  int brute_used;             /* bm_brute_used */
+  unsigned char brute_badmap[LSEC_MAX_DEVS];  /* badmap_brute */
+} lsec_inspect_state_t;
+int lsec_segment_inspect(lio_erasure_plan_t *plan, char *buf, int nstripes, int chunk, int flags,
+                         int *stripe_status, unsigned char *badmap, unsigned char *rewrite,
+                         lsec_inspect_state_t *state);
 
 /* Pre-build (and cache on the current device) the decode matrix for one erasure pattern,
  * so the first lsec_decode_dev of that pattern does no host work.  0 / -1. */

@@ -82,6 +82,19 @@ hipError_t launch_stripe_magic(const MagicArgs &a, hipStream_t stream);
 hipError_t launch_magic_finalize(const unsigned long long *acc, int nstripes, int64_t total_len, uint8_t *magic,
                                  hipStream_t stream);
 
+// Chunk comparison for the control-chunk check of jerase_control_check (segment/jerasure.c:
+// 202-269): flags[s] = 1 when any byte of a[p] and b[p] (p < npairs) differs in stripe s
+// (flags zeroed by the caller).
+struct DiffArgs {
+  int npairs;
+  int nstripes;
+  int64_t size;
+  int *flags;
+  ShardRef a[kMaxR];
+  ShardRef b[kMaxR];
+};
+hipError_t launch_chunk_diff(const DiffArgs &a, hipStream_t stream);
+
 // Host helper: fill one cell for coefficient c.
 void make_cell(uint8_t c, CoefCell &cell);
 

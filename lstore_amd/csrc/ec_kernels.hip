@@ -176,7 +176,48 @@ __global__ void k_magic_finalize(const unsigned long long *acc, int nstripes, ui
   magic[4 * s + 3] = m >> 24;
 }
 
+// one block per (stripe, 8 KiB column tile): OR of a^b over every pair, one flag store per
+// differing wave
+__global__ __launch_bounds__(kBlock) void k_chunk_diff(DiffArgs a) {
+  constexpr int kIt = 2, kTile = kBlock * 16 * kIt;
+  const int64_t C = a.size;
+  const uint32_t tps = static_cast<uint32_t>((C + kTile - 1) / kTile);
+  const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
+  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+    const uint32_t s = t / tps;
+    const int64_t off0 = static_cast<int64_t>(t - s * tps) * kTile + threadIdx.x * 16;
+    uint32_t d = 0;
+    for (int p = 0; p < a.npairs; ++p) {
+      const uint64_t pa = a.a[p].base + s * a.a[p].stride, pb = a.b[p].base + s * a.b[p].stride;
+#pragma unroll
+      for (int it = 0; it < kIt; ++it) {
+        const int64_t o = off0 + it * kBlock * 16;
+        if (o + 16 <= C) {
+          const u32x4 x = __builtin_nontemporal_load(gptr<u32x4>(pa + o));
+          const u32x4 y = __builtin_nontemporal_load(gptr<u32x4>(pb + o));
+          const u32x4 z = x ^ y;
+          d |= z.x | z.y | z.z | z.w;
+        } else if (o < C) {
+          const u32x2 x = *gptr<u32x2>(pa + o), y = *gptr<u32x2>(pb + o);
+          d |= (x.x ^ y.x) | (x.y ^ y.y);
+        }
+      }
+    }
+    if (__any(d != 0) && (threadIdx.x & 63) == 0) a.flags[s] = 1;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_chunk_diff(const DiffArgs &a, hipStream_t st) {
+  if (a.npairs < 1 || a.npairs > kMaxR || a.size % 8 != 0 || !a.flags) return hipErrorInvalidValue;
+  if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
+  const uint64_t tile = kBlock * 16 * 2;
+  const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
+  if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_chunk_diff, dim3(default_grid(ntiles)), dim3(kBlock), 0, st, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_stripe_magic(const MagicArgs &a, hipStream_t st) {
   if (a.nshards < 1 || a.nshards > kMaxMagicShards || a.size % 8 != 0) return hipErrorInvalidValue;

@@ -71,8 +71,20 @@ class ShardRef(C.Structure):
 EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan", "et_destroy_plan",
            "et_encode", "et_decode", "et_encode_stripes", "et_decode_stripes", "lsec_encode_dev",
            "lsec_decode_dev", "et_encode_stripes_magic", "et_stripes_magic", "lsec_encode_magic_dev",
-           "lsec_stripe_magic_dev", "lsec_segment_write", "lsec_segment_read", "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count",
-           "lsec_last_error", "lsec_plan_kernel", "lsec_set_kernel_variant")
+           "lsec_stripe_magic_dev", "lsec_segment_write", "lsec_segment_read", "lsec_segment_inspect",
+           "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count", "lsec_last_error", "lsec_plan_kernel",
+           "lsec_set_kernel_variant")
+
+# read / inspect flags and stripe states (include/lstore_ec.h)
+READ_PARANOID, MAGIC_LEGACY, INSPECT_FIX, MAX_DEVS = 1, 2, 4, 64
+STRIPE_OK, STRIPE_EMPTY, STRIPE_BAD_MAGIC, STRIPE_REPAIRED, STRIPE_LOST_MAGIC, STRIPE_LOST_MISMATCH = range(6)
+
+
+class InspectState(C.Structure):
+    """lsec_inspect_state_t: counters + the carried brute-force guess of one inspection."""
+    _fields_ = [("bad_stripes", C.c_longlong), ("unrecoverable", C.c_longlong), ("silent_errors", C.c_longlong),
+                ("empty_stripes", C.c_longlong), ("brute_used", C.c_int),
+                ("brute_badmap", C.c_ubyte * MAX_DEVS)]
 
 _lib = None
 
@@ -122,6 +134,8 @@ def lib():
     L.lsec_segment_write.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_void_p]
     L.lsec_segment_read.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_int, C.c_void_p,
                                     C.c_void_p]
+    L.lsec_segment_inspect.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.POINTER(InspectState)]
     L.lsec_last_error.restype = C.c_char_p
     L.lsec_plan_kernel.argtypes = [P]
     L.lsec_set_kernel_variant.argtypes = [C.c_int, C.c_int]
@@ -331,17 +345,37 @@ class Plan:
         return dev
 
     def segment_read(self, dev: np.ndarray, nstripes: int, chunk: int, n_shift: int = 1, first_stripe: int = 0,
-                     paranoid: bool = False, missing=()):
+                     paranoid: bool = False, missing=(), legacy_magic: bool = False):
         """device images uint8 [k+m, N*(C+4)] -> (data uint8 [N, k, C], status int32 [N], n_unrecoverable)."""
         n = self.k + self.m
         addrs = [0 if i in missing else dev[i].ctypes.data for i in range(n)]
         data = np.zeros((nstripes, self.k, chunk), dtype=np.uint8)
         status = np.zeros(nstripes, dtype=np.int32)
+        flags = (READ_PARANOID if paranoid else 0) | (MAGIC_LEGACY if legacy_magic else 0)
         bad = lib().lsec_segment_read(self._p, self._ptr_array(addrs), nstripes, chunk, n_shift, first_stripe,
-                                      int(paranoid), data.ctypes.data, status.ctypes.data)
+                                      flags, data.ctypes.data, status.ctypes.data)
         if bad < 0:
             raise ErasureError(f"lsec_segment_read failed: {last_error()}")
         return data, status, bad
+
+    def segment_inspect(self, buf: np.ndarray, chunk: int, fix: bool = False, legacy_magic: bool = False,
+                        state: "InspectState | None" = None):
+        """lsec_segment_inspect over buf uint8 [N, k+m, C+4] (stripe-major [magic | chunk] records,
+        repaired in place with fix=True) -> (status int32 [N], badmap uint8 [N, k+m],
+        rewrite uint8 [N, k+m], state)."""
+        n = self.k + self.m
+        if buf.ndim != 3 or buf.shape[1] != n or buf.shape[2] != chunk + 4 or not buf.flags.c_contiguous:
+            raise ValueError("buf must be a contiguous uint8 [N, k+m, C+4] array")
+        nstr = buf.shape[0]
+        status = np.zeros(nstr, np.int32)
+        badmap = np.zeros((nstr, n), np.uint8)
+        rewrite = np.zeros((nstr, n), np.uint8)
+        state = InspectState() if state is None else state
+        flags = (INSPECT_FIX if fix else 0) | (MAGIC_LEGACY if legacy_magic else 0)
+        _check(lib().lsec_segment_inspect(self._p, buf.ctypes.data, nstr, chunk, flags, status.ctypes.data,
+                                          badmap.ctypes.data, rewrite.ctypes.data, C.byref(state)),
+               "lsec_segment_inspect")
+        return status, badmap, rewrite, state
 
     # -- device-resident calls
     @staticmethod

@@ -83,6 +83,11 @@ def ref():
         lib.ref_segment_write.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong,
                                           C.c_void_p]
         lib.ref_segment_write.restype = None
+        lib.ref_segment_inspect.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.ref_segment_inspect.restype = None
+        lib.ref_segment_read.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_int,
+                                         C.c_int, C.c_void_p, C.c_void_p]
         _ref = lib
     return _ref
 
@@ -221,6 +226,30 @@ class RefPlan:
         data = np.ascontiguousarray(data)
         self.lib.ref_segment_write(self.h, data.ctypes.data, nstripes, chunk, n_shift, first_stripe, ptrs)
         return dev
+
+    def segment_inspect(self, buf, nstripes, chunk, magic_cksum=1, do_fix=0, brute=None):
+        """segjerase_inspect_full_func's per-stripe loop restated over the real jerasure (buf is
+        modified in place as the reference's buffer is).  Returns (status, badmap, rewrite,
+        counters[bad, unrecoverable, silent, empty], brute state)."""
+        n = self.k + self.m
+        status = np.zeros(nstripes, np.int32)
+        badmap = np.zeros((nstripes, n), np.uint8)
+        rewrite = np.zeros((nstripes, n), np.uint8)
+        counters = np.zeros(4, np.int64)
+        brute = np.zeros(1 + n, np.int32) if brute is None else brute
+        self.lib.ref_segment_inspect(self.h, buf.ctypes.data, nstripes, chunk, magic_cksum, do_fix, status.ctypes.data,
+                                     badmap.ctypes.data, rewrite.ctypes.data, counters.ctypes.data, brute.ctypes.data)
+        return status, badmap, rewrite, counters, brute
+
+    def segment_read(self, dev, nstripes, chunk, n_shift=1, first_stripe=0, paranoid=0, magic_cksum=1):
+        """segjerase_read_func's verification restated: (data [N,k,C], status, n_unrecoverable)."""
+        n = self.k + self.m
+        ptrs = _ptrs([dev[i] for i in range(n)])
+        data = np.zeros((nstripes, self.k, chunk), np.uint8)
+        status = np.zeros(nstripes, np.int32)
+        bad = self.lib.ref_segment_read(self.h, ptrs, nstripes, chunk, n_shift, first_stripe, paranoid, magic_cksum,
+                                        data.ctypes.data, status.ctypes.data)
+        return data, status, bad
 
     def encode_many(self, ptr_array, nstripes, size, nthreads):
         return self.lib.ref_plan_encode_many(self.h, ptr_array, nstripes, size, nthreads)

@@ -260,3 +260,243 @@ void ref_segment_write(ref_plan_t *p, const char *data, int nstripes, int chunk,
     free(parity);
     free(ptr);
 }
+
+/* ---------------------------------------------------------------- verification / repair
+ * The segment's verification helpers, restated over the real jerasure decode (ref_plan_decode)
+ * and zlib, since segment/jerasure.c cannot be built here:
+ *   h_cksum / h_cksum_cmp   je_cksum_calc / je_cksum_compare   (segment/jerasure.c:169-194)
+ *   h_control_check         jerase_control_check               (:202-269)
+ *   h_brute_recurse         jerase_brute_recurse               (:271-314)
+ *   h_brute_recovery        jerase_brute_recovery              (:321-339)
+ * ptr / eptr / pwork have the reference's roles: decode_block rebuilds the erased devices
+ * through eptr, which aliases ptr (the stripe buffer) except for control chunks and the
+ * brute-force work buffers. */
+static void h_cksum(unsigned char *magic, char **ptr, int n, int C)
+{
+    unsigned long ck = adler32(0L, Z_NULL, 0);
+    for (int i = 0; i < n; i++) ck = adler32(ck, (unsigned char *)ptr[i], C);
+    for (int i = 0; i < 4; i++) { magic[i] = ck & 255; ck >>= 8; }
+}
+
+static int h_cksum_cmp(const unsigned char *magic, char **ptr, int n, int C)
+{
+    unsigned char calc[4];
+    h_cksum(calc, ptr, n, C);
+    return memcmp(magic, calc, 4) == 0 ? 0 : 1;
+}
+
+static int h_control_check(ref_plan_t *p, int C, int n, int m, int *badmap, char **ptr, char **eptr, char **pwork,
+                           const unsigned char *magic)
+{
+    int erasures[n + 1], control[m + 1];
+    int nbad = 0;
+    for (int i = 0; i < n; i++) nbad += badmap[i];
+    if (magic && nbad == 0) return h_cksum_cmp(magic, ptr, n, C);   /* nothing to rebuild */
+    int n_ctl_max = magic ? 0 : m - nbad;
+    int control_index = -1, errors = 0;
+    do {
+        memcpy(eptr, ptr, sizeof(char *) * n);
+        int nc = 0, ne = 0;
+        for (int i = 0; i < n; i++) {
+            int take_ctl = !badmap[i] && nc < n_ctl_max && i > control_index;
+            if (!take_ctl && !badmap[i]) continue;
+            erasures[ne++] = i;
+            if (take_ctl) { control[nc] = i; eptr[i] = pwork[nc]; nc++; control_index = i; }
+        }
+        erasures[ne] = -1;
+        ref_plan_decode(p, eptr, C, erasures);
+        if (magic) return h_cksum_cmp(magic, eptr, n, C);
+        if (nc <= 0) {
+            if (n_ctl_max > 0) control_index = n - 1;
+            else return 0;                           /* m devices bad: nothing to compare */
+        }
+        for (int i = 0; i < nc; i++)
+            if (memcmp(ptr[control[i]], eptr[control[i]], C) != 0) return ++errors;
+    } while (control_index < n - 1);
+    return errors;
+}
+
+static int h_brute_recurse(int level, int *index, ref_plan_t *p, int C, int n, int m, int nbad, int *badmap, char **ptr,
+                           char **eptr, char **pwork, const unsigned char *magic)
+{
+    if (level == nbad) {   /* the combination is complete: swap in work buffers and check */
+        char *saved[m + 1];
+        memset(badmap, 0, sizeof(int) * n);
+        for (int i = 0; i < nbad; i++) { saved[i] = ptr[index[i]]; ptr[index[i]] = pwork[i]; badmap[index[i]] = 1; }
+        int r = h_control_check(p, C, n, m, badmap, ptr, eptr, pwork + nbad, magic);
+        for (int i = 0; i < nbad; i++) ptr[index[i]] = saved[i];
+        return r;
+    }
+    for (int i = level == 0 ? 0 : index[level - 1] + 1; i < n; i++) {
+        index[level] = i;
+        if (h_brute_recurse(level + 1, index, p, C, n, m, nbad, badmap, ptr, eptr, pwork, magic) == 0) return 0;
+    }
+    return 1;
+}
+
+static int h_brute_recovery(ref_plan_t *p, int C, int n, int m, int *badmap, char **ptr, char **eptr, char **pwork,
+                            const unsigned char *magic)
+{
+    int index[m + 1];
+    if (h_control_check(p, C, n, m, badmap, ptr, eptr, pwork, magic) == 0) return 0;   /* the given badmap */
+    memset(badmap, 0, sizeof(int) * n);
+    int ncheck = magic ? m + 1 : m;   /* with magic no control chunk is needed */
+    for (int e = 1; e < ncheck; e++) {
+        memset(index, 0, sizeof(index));
+        if (h_brute_recurse(0, index, p, C, n, m, e, badmap, ptr, eptr, pwork, magic) == 0) return 0;
+    }
+    return 1;
+}
+
+/* majority vote over the n magics at mag[j] (first group with the largest count wins):
+ * fills badmap with the devices outside the quorum, returns the quorum's count */
+static int h_quorum(int n, unsigned char **mag, int *badmap, unsigned char *qmagic)
+{
+    int group[n], count[n], ng = 0;
+    unsigned char *key[n];
+    for (int j = 0; j < n; j++) {
+        int g = 0;
+        while (g < ng && memcmp(key[g], mag[j], 4) != 0) g++;
+        if (g == ng) { key[ng] = mag[j]; count[ng] = 0; ng++; }
+        count[g]++;
+        group[j] = g;
+    }
+    int best = 0;
+    for (int g = 1; g < ng; g++) if (count[g] > count[best]) best = g;
+    for (int j = 0; j < n; j++) badmap[j] = group[j] != best;
+    memcpy(qmagic, key[best], 4);
+    return count[best];
+}
+
+static int h_nonzero(const char *b, int C) { for (int i = 0; i < C; i++) if (b[i]) return 1; return 0; }
+
+/* segjerase_inspect_full_func's per-stripe loop (segment/jerasure.c:473-660) over one
+ * buffer: nstripes x (k+m) records of [4-byte magic | chunk].  status[s] uses the engine's
+ * LSEC_STRIPE_* numbering (0 ok, 1 empty, 2 bad magic, 3 repaired, 4 lost: magic,
+ * 5 lost: mismatch); badmap_out / rewrite as lsec_segment_inspect documents.
+ * counters[4] += bad_count, unrecoverable_count, erasure_errors, n_empty;
+ * brute[0] / brute[1..n] = bm_brute_used / badmap_brute, carried between calls. */
+void ref_segment_inspect(ref_plan_t *p, char *buf, int nstripes, int chunk, int magic_cksum, int do_fix, int *status,
+                         unsigned char *badmap_out, unsigned char *rewrite, long long *counters, int *brute)
+{
+    int k = p->k, m = p->m, n = k + m, C = chunk;
+    size_t rec = (size_t)C + 4;
+    int badmap[n];
+    char *ptr[n], *eptr[n], *pwork[m];
+    unsigned char *mag[n], qmagic[4], zero[4] = {0, 0, 0, 0};
+    char *parity = (char *)malloc((size_t)m * C);
+    for (int i = 0; i < m; i++) pwork[i] = parity + (size_t)i * C;
+    memset(rewrite, do_fix && !magic_cksum ? 1 : 0, (size_t)nstripes * n);   /* legacy: whole range (:464-470) */
+    for (int s = 0; s < nstripes; s++) {
+        char *b = buf + (size_t)s * n * rec;
+        for (int j = 0; j < n; j++) { mag[j] = (unsigned char *)(b + j * rec); ptr[j] = b + j * rec + 4; }
+        int count = h_quorum(n, mag, badmap, qmagic);
+        int good_magic = memcmp(zero, qmagic, 4) != 0, skip = 0, st;
+        if (!good_magic) {
+            int nz = 0;
+            for (int j = 0; j < n && !nz; j++) nz = h_nonzero(ptr[j], C);
+            if (nz) good_magic = 1;
+            else if (count == n) { counters[3]++; status[s] = 1;
+                                   for (int j = 0; j < n; j++) badmap_out[(size_t)s * n + j] = badmap[j]; continue; }
+        }
+        const unsigned char *check_magic = magic_cksum ? qmagic : NULL;
+        if ((!good_magic && count != n) || count < k) {
+            counters[1]++; counters[0]++;
+            st = 4;
+        } else {
+            if (h_control_check(p, C, n, m, badmap, ptr, eptr, pwork, check_magic) != 0) {
+                counters[0]++; counters[2]++;
+                if (brute[0]) for (int j = 0; j < n; j++) badmap[j] = brute[1 + j];
+                if (h_brute_recovery(p, C, n, m, badmap, ptr, eptr, pwork, check_magic) == 0) {
+                    brute[0] = 1;
+                    for (int j = 0; j < n; j++) brute[1 + j] = badmap[j];
+                    st = 3;
+                } else {
+                    st = 5; skip = 1; counters[1]++;
+                }
+            } else if (count != n) {
+                counters[0]++; st = 2;
+            } else {
+                st = 0;
+                if (magic_cksum) skip = 1;
+            }
+            if (!skip && do_fix) {
+                unsigned char newmagic[4];
+                const unsigned char *wm = qmagic;
+                if (!magic_cksum) { h_cksum(newmagic, eptr, n, C); wm = newmagic; }
+                for (int j = 0; j < n; j++) {
+                    if (!badmap[j] && magic_cksum) continue;
+                    memcpy(b + j * rec, wm, 4);
+                    if (eptr[j] != ptr[j]) memcpy(ptr[j], eptr[j], C);
+                    if (magic_cksum) rewrite[(size_t)s * n + j] = 1;
+                }
+            }
+        }
+        status[s] = st;
+        for (int j = 0; j < n; j++) badmap_out[(size_t)s * n + j] = badmap[j];
+    }
+    free(parity);
+}
+
+/* segjerase_read_func's per-stripe verification (segment/jerasure.c:1378-1505) over device
+ * images laid out as ref_segment_write makes them (every device readable).  status[s] =
+ * 0 ok, 1 recovered, 2 blank, -1 unrecoverable, as lsec_segment_read reports; returns the
+ * number of unrecoverable stripes. */
+int ref_segment_read(ref_plan_t *p, char **dev, int nstripes, int chunk, int n_shift, long long first_stripe,
+                     int paranoid, int magic_cksum, char *data_out, int *status)
+{
+    int k = p->k, m = p->m, n = k + m, C = chunk, bad = 0, brute_used = 0;
+    size_t rec = (size_t)C + 4;
+    int badmap[n], badmap_brute[n];
+    char *ptr[n], *eptr[n], *pwork[m];
+    unsigned char *mag[n], qmagic[4], zero[4] = {0, 0, 0, 0};
+    char *work = (char *)malloc((size_t)n * C), *parity = (char *)malloc((size_t)m * C);
+    for (int i = 0; i < m; i++) pwork[i] = parity + (size_t)i * C;
+    for (int s = 0; s < nstripes; s++) {
+        long long ss = first_stripe + s;
+        for (int j = 0; j < n; j++) {   /* logical chunk j from device (j - ss*n_shift) mod n (lun.c:1178-1223) */
+            int d = (int)(((j - ss * n_shift) % n + n) % n);
+            char *r = dev[d] + (size_t)s * rec;
+            mag[j] = (unsigned char *)r;
+            ptr[j] = work + (size_t)j * C;
+            memcpy(ptr[j], r + 4, C);
+        }
+        int count = h_quorum(n, mag, badmap, qmagic), data_ok = 1, st = 0;
+        if (count != n) {
+            int nd = 0;
+            for (int j = 0; j < n; j++) nd += !badmap[j] && j < k;
+            if (nd != k) data_ok = 0;
+        } else if (memcmp(zero, qmagic, 4) == 0) {
+            int nz = 0;
+            for (int j = 0; j < n && !nz; j++) nz = h_nonzero(ptr[j], C);
+            data_ok = nz ? 1 : 2;
+        }
+        int recover = 0;
+        if (data_ok == 1) recover = paranoid;
+        else if (data_ok == 2) { memset(work, 0, (size_t)k * C); st = 2; }
+        else if (count < k) st = -1;
+        else recover = 1;
+        if (recover) {
+            const unsigned char *cm = magic_cksum ? qmagic : NULL;
+            if (h_control_check(p, C, n, m, badmap, ptr, eptr, pwork, cm) != 0) {
+                if (brute_used) memcpy(badmap, badmap_brute, sizeof(badmap));
+                if (h_brute_recovery(p, C, n, m, badmap, ptr, eptr, pwork, cm) == 0) {
+                    brute_used = 1;
+                    memcpy(badmap_brute, badmap, sizeof(badmap));
+                    for (int j = 0; j < k; j++) if (eptr[j] != ptr[j]) memcpy(ptr[j], eptr[j], C);
+                    for (int j = 0; j < k; j++) if (badmap[j]) st = 1;   /* user data rebuilt */
+                } else {
+                    st = -1;
+                }
+            } else {
+                for (int j = 0; j < k; j++) if (badmap[j]) st = 1;
+            }
+        }
+        status[s] = st;
+        if (st == -1) bad++;
+        else memcpy(data_out + (size_t)s * k * C, work, (size_t)k * C);
+    }
+    free(work);
+    free(parity);
+    return bad;
+}
