@@ -37,14 +37,15 @@ hipError_t by_r(int R, F f) {
 }
 
 // Launch shape for a K x R bytewise launch (codes in ec_kernels_impl.h).  variant 0 = the
-// automatic policy measured with tools/kbench.py (profiles/r01_v3_kbench_vw.txt):
-//   R == 1 (single-erasure decode: XOR-heavy, read-bound)  8 B per lane        (+1.5-2 %)
-//   K*R >= 48 (wide encodes: VALU-heavy, register-bound)    2 x 8 B per lane    (+6-9 %)
-//   otherwise                                                2 x 16 B per lane
+// automatic policy measured with tools/kbench.py (profiles/r01_v6_kbench_branchfree.txt):
+//   R == 1 (single-erasure decode: XOR-heavy, read-bound)  8 B per lane, branchy cells
+//   otherwise                                                2 x 16 B per lane, branch-free
+//                                                            (RS 20+6 encode 52 -> 62 %,
+//                                                            8+4 / 10+4 +3 points)
 int bytewise_shape(int K, int R) {
+  (void)K;
   if (g_bw_variant > 0) return (g_bw_variant - 1) % kBwShapes;
-  if (R == 1) return 3;
-  return K * R >= 48 ? 2 : 0;
+  return R == 1 ? 4 : 0;
 }
 
 }  // namespace

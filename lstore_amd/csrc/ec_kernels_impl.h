@@ -152,6 +152,70 @@ __device__ __forceinline__ void bw_accumulate(typename VecT<VW>::type (&acc)[IT]
   }
 }
 
+// Branch-free variant: every coefficient takes the 3-perm path (the tables of 0 and 1 give 0
+// and the identity), so there are no per-cell branches (whose merges cost register copies
+// and serialise the cell loads), and inputs are taken two at a time so three 3-input XORs
+// fold six partial products.  The c*(v>>6) table has 4 entries: one dword, so that perm
+// takes an inline 0 as its high half and needs no VGPR copy of the table.
+template <int IT, int VW>
+__device__ __forceinline__ void bw_fields(const typename VecT<VW>::type (&v)[IT], typename VecT<VW>::type (&fa)[IT],
+                                          typename VecT<VW>::type (&fb)[IT], typename VecT<VW>::type (&fc)[IT]) {
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    fa[it] = v[it] & 0x07070707u;
+    fb[it] = (v[it] >> 3) & 0x07070707u;
+    fc[it] = (v[it] >> 6) & 0x03030303u;
+  }
+}
+
+template <int R, int IT, int VW, bool TWO>
+__device__ __forceinline__ void bw_accumulate_bf(typename VecT<VW>::type (&acc)[IT][R],
+                                                 const typename VecT<VW>::type (&va)[IT],
+                                                 const typename VecT<VW>::type (&vb)[IT], ConstCell *cells, int K, int j) {
+  typedef typename VecT<VW>::type V;
+  V ia[IT], ib[IT], ic[IT], ja[IT], jb[IT], jc[IT];
+  bw_fields<IT, VW>(va, ia, ib, ic);
+  if constexpr (TWO) bw_fields<IT, VW>(vb, ja, jb, jc);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    ConstCell *ca = cells + r * K + j;  // wave-uniform -> scalar loads
+    const uint32_t a0 = ca->ta_lo, a1 = ca->ta_hi, a2 = ca->tb_lo, a3 = ca->tb_hi, a4 = ca->tc_lo;
+    uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0, b4 = 0;
+    if constexpr (TWO) {
+      ConstCell *cb = ca + 1;
+      b0 = cb->ta_lo, b1 = cb->ta_hi, b2 = cb->tb_lo, b3 = cb->tb_hi, b4 = cb->tc_lo;
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+#pragma unroll
+      for (int e = 0; e < VW; ++e) {
+        uint32_t x = acc[it][r][e];
+        const uint32_t p1 = __builtin_amdgcn_perm(a1, a0, ia[it][e]);
+        const uint32_t p2 = __builtin_amdgcn_perm(a3, a2, ib[it][e]);
+        const uint32_t p3 = __builtin_amdgcn_perm(0u, a4, ic[it][e]);
+        if constexpr (TWO) {
+          const uint32_t q1 = __builtin_amdgcn_perm(b1, b0, ja[it][e]);
+          const uint32_t q2 = __builtin_amdgcn_perm(b3, b2, jb[it][e]);
+          const uint32_t q3 = __builtin_amdgcn_perm(0u, b4, jc[it][e]);
+          x = xor3(x, p1, p2);
+          x = xor3(x, p3, q1);
+          x = xor3(x, q2, q3);
+        } else {
+          x = xor3(x, p1, p2) ^ p3;
+        }
+        acc[it][r][e] = x;
+      }
+  }
+}
+
+// one input (BF = false: branchy per-cell path; true: branch-free)
+template <int R, int IT, int VW, bool BF>
+__device__ __forceinline__ void bw_acc1(typename VecT<VW>::type (&acc)[IT][R], const typename VecT<VW>::type (&v)[IT],
+                                       ConstCell *cells, int K, int j) {
+  if constexpr (BF) bw_accumulate_bf<R, IT, VW, false>(acc, v, v, cells, K, j);
+  else bw_accumulate<R, IT, VW>(acc, v, cells, K, j);
+}
+
 // fused stripe magic: every lane adds its bytes' position-weighted sums, the block reduces
 // them and adds one pair per tile into the stripe's accumulator
 template <int R, int IT, int VW>
@@ -187,10 +251,10 @@ __device__ __forceinline__ void magic_commit(unsigned long long *acc, uint32_t s
   }
 }
 
-// MINW = minimum waves per SIMD the register allocation must allow (1 = unconstrained).
+// BF = branch-free coefficient path (bw_accumulate_bf).
 // MG = also accumulate the stripe magic of inputs + outputs (encode + je_cksum_calc fused).
-template <int R, int KC, int IT, int MINW, int VW, bool MG = false>
-__global__ __launch_bounds__(kBlock, MINW) void k_gf8_bytewise(ApplyArgs a) {
+template <int R, int KC, int IT, bool BF, int VW, bool MG = false>
+__global__ __launch_bounds__(kBlock) void k_gf8_bytewise(ApplyArgs a) {
   typedef typename VecT<VW>::type V;
   __shared__ uint32_t red[MG ? kBlock / 64 : 1];
   constexpr int kStep = BwTile<IT, VW>::kStep;
@@ -224,8 +288,14 @@ __global__ __launch_bounds__(kBlock, MINW) void k_gf8_bytewise(ApplyArgs a) {
 #pragma unroll
           for (int it = 0; it < IT; ++it) v[j][it] = __builtin_nontemporal_load(gptr<V>(p + it * kStep));
         }
+        if constexpr (BF) {
 #pragma unroll
-        for (int j = 0; j < KC; ++j) bw_accumulate<R, IT, VW>(acc, v[j], cells, K, j);
+          for (int j = 0; j + 1 < KC; j += 2) bw_accumulate_bf<R, IT, VW, true>(acc, v[j], v[j + 1], cells, K, j);
+          if constexpr (KC % 2) bw_accumulate_bf<R, IT, VW, false>(acc, v[KC - 1], v[KC - 1], cells, K, KC - 1);
+        } else {
+#pragma unroll
+          for (int j = 0; j < KC; ++j) bw_accumulate<R, IT, VW>(acc, v[j], cells, K, j);
+        }
         if constexpr (MG) bw_magic<R, IT, VW>(a, s, off0, K, v, KC, 0, mas, mbs);
       } else {
         for (int j0 = 0; j0 < K; j0 += 4) {
@@ -239,9 +309,15 @@ __global__ __launch_bounds__(kBlock, MINW) void k_gf8_bytewise(ApplyArgs a) {
               for (int it = 0; it < IT; ++it) v[jj][it] = __builtin_nontemporal_load(gptr<V>(p + it * kStep));
             }
           }
+          if constexpr (BF) {
+            if (nj >= 2) bw_accumulate_bf<R, IT, VW, true>(acc, v[0], v[1], cells, K, j0);
+            if (nj == 4) bw_accumulate_bf<R, IT, VW, true>(acc, v[2], v[3], cells, K, j0 + 2);
+            if (nj == 1 || nj == 3) bw_accumulate_bf<R, IT, VW, false>(acc, v[nj - 1], v[nj - 1], cells, K, j0 + nj - 1);
+          } else {
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj)
-            if (jj < nj) bw_accumulate<R, IT, VW>(acc, v[jj], cells, K, j0 + jj);
+            for (int jj = 0; jj < 4; ++jj)
+              if (jj < nj) bw_accumulate<R, IT, VW>(acc, v[jj], cells, K, j0 + jj);
+          }
           if constexpr (MG) bw_magic<R, IT, VW>(a, s, off0, K, v, nj, j0, mas, mbs);
         }
       }
@@ -268,7 +344,7 @@ __global__ __launch_bounds__(kBlock, MINW) void k_gf8_bytewise(ApplyArgs a) {
             v[it][1] = h.y;
           }
         }
-        bw_accumulate<R, IT, VW>(acc, v, cells, K, j);
+        bw_acc1<R, IT, VW, BF>(acc, v, cells, K, j);
         if constexpr (MG) {
           const V(*vv)[IT] = &v;
           bw_magic<R, IT, VW>(a, s, off0, K, vv, 1, j, mas, mbs);
@@ -513,32 +589,35 @@ __global__ __launch_bounds__(kBlock) void k_gfw_wordwise(ApplyArgs a) {
                             X(18) X(19) X(22) X(23) X(28) X(29) X(30) X(31) X(32)
 
 // ------------------------------------------------------------------ per-R dispatch
-template <int R, int IT, int MINW, int VW>
+template <int R, int IT, bool BF, int VW>
 hipError_t bytewise_k(const ApplyArgs &a, hipStream_t st, int grid) {
   switch (a.K) {
 #define LSEC_BW_K(KK) \
-  case KK: hipLaunchKernelGGL((k_gf8_bytewise<R, KK, IT, MINW, VW>), dim3(grid), dim3(kBlock), 0, st, a); break;
+  case KK: hipLaunchKernelGGL((k_gf8_bytewise<R, KK, IT, BF, VW>), dim3(grid), dim3(kBlock), 0, st, a); break;
     LSEC_BW_K(4) LSEC_BW_K(6) LSEC_BW_K(8) LSEC_BW_K(10) LSEC_BW_K(12) LSEC_BW_K(16) LSEC_BW_K(20)
 #undef LSEC_BW_K
-    default: hipLaunchKernelGGL((k_gf8_bytewise<R, 0, IT, MINW, VW>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    default: hipLaunchKernelGGL((k_gf8_bytewise<R, 0, IT, BF, VW>), dim3(grid), dim3(kBlock), 0, st, a); break;
   }
   return hipGetLastError();
 }
 
-// Bytewise launch shapes (tile per lane):  code -> (IT, VW)   [all MINW = 1]
-//   0 -> (2, 4) 32 B/lane    1 -> (1, 4) 16 B/lane    2 -> (2, 2) 16 B/lane in 8 B pieces
-//   3 -> (1, 2)  8 B/lane
-constexpr int kBwShapes = 4;
+// Bytewise launch shapes (tile per lane):  code -> (IT, VW, coefficient path)
+//   0 -> (2, 4) 32 B/lane, branch-free   1 -> (1, 4) 16 B/lane, branch-free
+//   2 -> (2, 2) 16 B/lane in 8 B pieces, branch-free   3 -> (1, 2) 8 B/lane, branch-free
+//   4 -> (1, 2) 8 B/lane, per-cell branches (single-output decodes: mostly XORs of
+//        coefficient-1 inputs, which the branch turns into one v_xor instead of 3 perms)
+constexpr int kBwShapes = 5;
 inline int bw_shape_it(int shape) { return (shape == 0 || shape == 2) ? 2 : 1; }
 inline int bw_shape_vw(int shape) { return shape <= 1 ? 4 : 2; }
 
 template <int R>
 hipError_t dispatch_bytewise(const ApplyArgs &a, hipStream_t st, int grid, int shape) {
   switch (shape) {
-    case 1: return bytewise_k<R, 1, 1, 4>(a, st, grid);
-    case 2: return bytewise_k<R, 2, 1, 2>(a, st, grid);
-    case 3: return bytewise_k<R, 1, 1, 2>(a, st, grid);
-    default: return bytewise_k<R, 2, 1, 4>(a, st, grid);
+    case 1: return bytewise_k<R, 1, true, 4>(a, st, grid);
+    case 2: return bytewise_k<R, 2, true, 2>(a, st, grid);
+    case 3: return bytewise_k<R, 1, true, 2>(a, st, grid);
+    case 4: return bytewise_k<R, 1, false, 2>(a, st, grid);
+    default: return bytewise_k<R, 2, true, 4>(a, st, grid);
   }
 }
 
@@ -546,10 +625,10 @@ template <int R>
 hipError_t dispatch_bytewise_magic(const ApplyArgs &a, hipStream_t st, int grid) {
   switch (a.K) {
 #define LSEC_BWM_K(KK) \
-  case KK: hipLaunchKernelGGL((k_gf8_bytewise<R, KK, 2, 1, 4, true>), dim3(grid), dim3(kBlock), 0, st, a); break;
+  case KK: hipLaunchKernelGGL((k_gf8_bytewise<R, KK, 2, true, 4, true>), dim3(grid), dim3(kBlock), 0, st, a); break;
     LSEC_BWM_K(4) LSEC_BWM_K(6) LSEC_BWM_K(8) LSEC_BWM_K(10) LSEC_BWM_K(12) LSEC_BWM_K(16) LSEC_BWM_K(20)
 #undef LSEC_BWM_K
-    default: hipLaunchKernelGGL((k_gf8_bytewise<R, 0, 2, 1, 4, true>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    default: hipLaunchKernelGGL((k_gf8_bytewise<R, 0, 2, true, 4, true>), dim3(grid), dim3(kBlock), 0, st, a); break;
   }
   return hipGetLastError();
 }
