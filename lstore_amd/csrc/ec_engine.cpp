@@ -698,19 +698,6 @@ void release_staging(Staging *s) {
   g_pool[s->dev].push_back(s);
 }
 
-int ensure_slot(Staging::Slot &sl, size_t bytes) {
-  if (sl.cap >= bytes) return 0;
-  if (sl.d) (void)hipFree(sl.d);
-  if (sl.h) (void)hipHostFree(sl.h);
-  sl.d = nullptr;
-  sl.h = nullptr;
-  sl.cap = 0;
-  HIP_OK(hipMalloc(&sl.d, bytes));
-  HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&sl.h), bytes, hipHostMallocDefault));
-  sl.cap = bytes;
-  return 0;
-}
-
 size_t staging_budget() {
   static size_t b = [] {
     const char *s = getenv("LSEC_STAGING_MB");
@@ -718,6 +705,74 @@ size_t staging_budget() {
     return static_cast<size_t>(std::max(1L, v)) << 20;
   }();
   return b;
+}
+
+// Slots are sized for a full batch (half the staging budget) the first time, so that a
+// small first call does not leave them too small for the next one: re-pinning 64 MiB of
+// host memory costs more than moving it over PCIe.  need_host = false (pinned callers, see
+// below) allocates only the device half.
+int ensure_slot(Staging::Slot &sl, size_t bytes, bool need_host = true) {
+  if (sl.cap >= bytes && (sl.h || !need_host)) return 0;
+  if (sl.d) (void)hipFree(sl.d);
+  if (sl.h) (void)hipHostFree(sl.h);
+  sl.d = nullptr;
+  sl.h = nullptr;
+  sl.cap = 0;
+  const size_t cap = std::max(bytes, staging_budget() / 2);
+  HIP_OK(hipMalloc(&sl.d, cap));
+  if (need_host) HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&sl.h), cap, hipHostMallocDefault));
+  sl.cap = cap;
+  return 0;
+}
+
+// Caller buffers that are already page-locked (hipHostMalloc'd, or hipHostRegister'ed by an
+// allocator that pins its cache pages) need no packing: the DMA engines copy straight
+// between them and the device slots, and the host copy pool stays idle.
+bool is_pinned_host(const void *ptr) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, ptr) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost;
+}
+
+// every staged shard of the first and last stripe pinned?  (a stray pageable pointer in
+// between stays correct -- hipMemcpyAsync accepts pageable memory too, only slower)
+bool pinned_layout(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids) {
+  static const bool off = getenv("LSEC_NO_PINNED_DMA") != nullptr;
+  if (off) return false;
+  for (int s : {0, nstripes - 1}) {
+    for (int id : in_ids)
+      if (!is_pinned_host(ptrs[static_cast<size_t>(s) * km + id])) return false;
+    for (int id : out_ids)
+      if (!is_pinned_host(ptrs[static_cast<size_t>(s) * km + id])) return false;
+  }
+  return true;
+}
+
+// DMA runs: pieces whose source and destination both continue the previous piece merge
+// into one copy (LStore's k data chunks of a stripe sit back to back in one cache page, so
+// a stripe's inputs usually become a single k*C transfer)
+struct DmaRun {
+  char *dst;
+  const char *src;
+  size_t bytes;
+};
+
+void add_run(std::vector<DmaRun> &v, char *dst, const char *src, size_t n) {
+  if (!v.empty() && v.back().dst + v.back().bytes == dst && v.back().src + v.back().bytes == src)
+    v.back().bytes += n;
+  else
+    v.push_back({dst, src, n});
+}
+
+hipError_t issue_runs(const std::vector<DmaRun> &v, hipMemcpyKind kind, hipStream_t st) {
+  for (const DmaRun &r : v) {
+    const hipError_t e = hipMemcpyAsync(r.dst, r.src, r.bytes, kind, st);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // Shared driver of the host-memory paths.  For each stripe, `in_ids` name the shards that
@@ -772,10 +827,15 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
     dmagic = reinterpret_cast<uint8_t *>(dacc + 2ull * nstripes);
   }
 
+  // pinned callers: DMA straight between their buffers and the device slots
+  const bool pinned = pinned_layout(ptrs, nstripes, km, in_ids, out_ids);
+  std::vector<DmaRun> runs;
+
   auto unpack = [&](Staging::Slot &sl) -> int {
     if (!sl.pending) return 0;
     sl.pending = false;
     if (hipEventSynchronize(sl.done) != hipSuccess) return fail("staging event sync failed");
+    if (pinned) return 0;  // the D2H already landed in the caller's buffers
     const size_t len = static_cast<size_t>(sl.clen);
     const char *outb = sl.h + static_cast<size_t>(sl.nb) * nin * len;
     jobs.clear();
@@ -795,16 +855,26 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
       const size_t len = static_cast<size_t>(clen);
       Staging::Slot &sl = stg->slot[which];
       if ((rc = unpack(sl))) break;
-      if ((rc = ensure_slot(sl, slot_bytes))) break;
-      jobs.clear();
-      for (int s = 0; s < nb; ++s)
-        for (int j = 0; j < nin; ++j)
-          jobs.push_back({sl.h + (static_cast<size_t>(s) * nin + j) * len,
-                          ptrs[static_cast<size_t>(s0 + s) * km + in_ids[j]] + c0, len});
-      CopyPool::get().run(jobs);
+      if ((rc = ensure_slot(sl, slot_bytes, !pinned))) break;
       const size_t in_bytes = static_cast<size_t>(nb) * nin * len;
       const size_t out_off = in_bytes;
-      hipError_t err = hipMemcpyAsync(sl.d, sl.h, in_bytes, hipMemcpyHostToDevice, stg->s_in);
+      hipError_t err;
+      if (pinned) {
+        runs.clear();
+        for (int s = 0; s < nb; ++s)
+          for (int j = 0; j < nin; ++j)
+            add_run(runs, sl.d + (static_cast<size_t>(s) * nin + j) * len, ptrs[static_cast<size_t>(s0 + s) * km + in_ids[j]] + c0,
+                    len);
+        err = issue_runs(runs, hipMemcpyHostToDevice, stg->s_in);
+      } else {
+        jobs.clear();
+        for (int s = 0; s < nb; ++s)
+          for (int j = 0; j < nin; ++j)
+            jobs.push_back({sl.h + (static_cast<size_t>(s) * nin + j) * len,
+                            ptrs[static_cast<size_t>(s0 + s) * km + in_ids[j]] + c0, len});
+        CopyPool::get().run(jobs);
+        err = hipMemcpyAsync(sl.d, sl.h, in_bytes, hipMemcpyHostToDevice, stg->s_in);
+      }
       if (err == hipSuccess) err = hipEventRecord(sl.in_done, stg->s_in);
       if (err == hipSuccess) err = hipStreamWaitEvent(stg->s_out, sl.in_done, 0);
       if (err != hipSuccess) { rc = fail("H2D: %s", hipGetErrorString(err)); break; }
@@ -827,7 +897,17 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
         err = lsec::launch_stripe_magic(ma, stg->s_out);
         if (err != hipSuccess) { rc = fail("magic launch: %s", hipGetErrorString(err)); break; }
       }
-      if (nout > 0) err = hipMemcpyAsync(sl.h + out_off, sl.d + out_off, static_cast<size_t>(nb) * nout * len, hipMemcpyDeviceToHost, stg->s_out);
+      if (nout > 0 && pinned) {
+        runs.clear();
+        for (int s = 0; s < nb; ++s)
+          for (int r = 0; r < nout; ++r)
+            add_run(runs, ptrs[static_cast<size_t>(s0 + s) * km + out_ids[r]] + c0,
+                    sl.d + out_off + (static_cast<size_t>(s) * nout + r) * len, len);
+        err = issue_runs(runs, hipMemcpyDeviceToHost, stg->s_out);
+      } else if (nout > 0) {
+        err = hipMemcpyAsync(sl.h + out_off, sl.d + out_off, static_cast<size_t>(nb) * nout * len, hipMemcpyDeviceToHost,
+                             stg->s_out);
+      }
       if (err == hipSuccess) err = hipEventRecord(sl.done, stg->s_out);
       if (err != hipSuccess) { rc = fail("D2H: %s", hipGetErrorString(err)); break; }
       sl.pending = true;
@@ -912,6 +992,7 @@ hipStream_t thread_stream() {
 struct HostReq {
   char **ptrs = nullptr;
   int nstripes = 0, km = 0, kind = 0, packet = 0, w = 8;
+  bool pinned = false;  // caller buffers page-locked: DMA in place, no packing
   long long C = 0;
   std::vector<int> in_ids, out_ids;
   const void *image = nullptr;
@@ -996,6 +1077,7 @@ class Dispatcher {
         const char *outb = sl.h + g.off + static_cast<size_t>(g.nstripes) * nin * C;
         for (size_t q = 0; q < g.reqs.size(); ++q) {
           const HostReq &r = *g.reqs[q];
+          if (r.pinned) continue;  // its D2H went straight into its buffers
           for (int s = 0; s < r.nstripes; ++s)
             for (size_t o = 0; o < nout; ++o)
               jobs.push_back({r.ptrs[static_cast<size_t>(s) * r.km + r.out_ids[o]],
@@ -1052,28 +1134,45 @@ class Dispatcher {
         return;
       sl.cap = cap;
     }
+    // Inputs: pageable requests are packed into the pinned slot and leave in one DMA per run
+    // of neighbouring requests; pinned requests are DMA'd from their own buffers.  Outputs
+    // mirror that (finish() unpacks only the pageable ones).
     std::vector<CopyJob> jobs;
+    std::vector<DmaRun> h2d, d2h;
     for (const Group &g : sl.groups) {
       const HostReq &r0 = *g.reqs[0];
-      const size_t C = static_cast<size_t>(r0.C), nin = r0.in_ids.size();
+      const size_t C = static_cast<size_t>(r0.C), nin = r0.in_ids.size(), nout = r0.out_ids.size();
+      const size_t out0 = g.off + static_cast<size_t>(g.nstripes) * nin * C;
       for (size_t q = 0; q < g.reqs.size(); ++q) {
         const HostReq &r = *g.reqs[q];
-        for (int s = 0; s < r.nstripes; ++s)
-          for (size_t j = 0; j < nin; ++j)
-            jobs.push_back({sl.h + g.off + ((static_cast<size_t>(g.first[q]) + s) * nin + j) * C,
-                            r.ptrs[static_cast<size_t>(s) * r.km + r.in_ids[j]], C});
+        const size_t ib = g.off + static_cast<size_t>(g.first[q]) * nin * C;
+        const size_t ob = out0 + static_cast<size_t>(g.first[q]) * nout * C;
+        if (r.pinned) {
+          for (int s = 0; s < r.nstripes; ++s) {
+            for (size_t j = 0; j < nin; ++j)
+              add_run(h2d, sl.d + ib + (static_cast<size_t>(s) * nin + j) * C, r.ptrs[static_cast<size_t>(s) * r.km + r.in_ids[j]], C);
+            for (size_t o = 0; o < nout; ++o)
+              add_run(d2h, r.ptrs[static_cast<size_t>(s) * r.km + r.out_ids[o]], sl.d + ob + (static_cast<size_t>(s) * nout + o) * C, C);
+          }
+        } else {
+          for (int s = 0; s < r.nstripes; ++s)
+            for (size_t j = 0; j < nin; ++j)
+              jobs.push_back({sl.h + ib + (static_cast<size_t>(s) * nin + j) * C, r.ptrs[static_cast<size_t>(s) * r.km + r.in_ids[j]], C});
+          add_run(h2d, sl.d + ib, sl.h + ib, static_cast<size_t>(r.nstripes) * nin * C);
+          add_run(d2h, sl.h + ob, sl.d + ob, static_cast<size_t>(r.nstripes) * nout * C);
+        }
       }
     }
     CopyPool::get().run(jobs);
+    if (!hip_err(issue_runs(h2d, hipMemcpyHostToDevice, s_in_), "H2D")) return;
+    if (!hip_err(hipEventRecord(in_done_, s_in_), "event") || !hip_err(hipStreamWaitEvent(s_out_, in_done_, 0), "wait"))
+      return;
     for (const Group &g : sl.groups) {
       const HostReq &r0 = *g.reqs[0];
       const size_t C = static_cast<size_t>(r0.C);
       const int nin = static_cast<int>(r0.in_ids.size()), nout = static_cast<int>(r0.out_ids.size());
       const size_t in_bytes = static_cast<size_t>(g.nstripes) * nin * C;
       char *dbase = sl.d + g.off;
-      if (!hip_err(hipMemcpyAsync(dbase, sl.h + g.off, in_bytes, hipMemcpyHostToDevice, s_in_), "H2D")) return;
-      if (!hip_err(hipEventRecord(in_done_, s_in_), "event") || !hip_err(hipStreamWaitEvent(s_out_, in_done_, 0), "wait"))
-        return;
       ShardRef in[lsec::kMaxK], out[64];
       for (int j = 0; j < nin; ++j)
         in[j] = {reinterpret_cast<uint64_t>(dbase) + static_cast<uint64_t>(j) * C, static_cast<int64_t>(nin * C)};
@@ -1083,10 +1182,8 @@ class Dispatcher {
         if (sl.err.empty()) sl.err = tl_err;
         return;
       }
-      if (!hip_err(hipMemcpyAsync(sl.h + g.off + in_bytes, dbase + in_bytes, static_cast<size_t>(g.nstripes) * nout * C,
-                                  hipMemcpyDeviceToHost, s_out_), "D2H"))
-        return;
     }
+    if (!hip_err(issue_runs(d2h, hipMemcpyDeviceToHost, s_out_), "D2H")) return;
     hip_err(hipEventRecord(sl.done, s_out_), "event");
   }
 
@@ -1156,6 +1253,7 @@ int run_coalesced(PlanExt *e, char **ptrs, int nstripes, long long C, const std:
   r.kind = kind;
   r.packet = e->pub.packet_size;
   r.w = e->pub.w;
+  r.pinned = pinned_layout(ptrs, nstripes, r.km, in_ids, out_ids);
   return Dispatcher::for_device(dev)->run(r);
 }
 

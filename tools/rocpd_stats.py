@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Kernel-trace summary from a rocprofv3 rocpd database (the default output on ROCm 7.2).
+
+python tools/rocpd_stats.py gpurun_out/prof_x/run_results.db [out.csv] [--all]
+
+Writes Name,GridX,Calls,AverageNs,MinNs,MaxNs,VGPRs,SGPRs per (kernel, grid) -- the same
+columns as the profiles/*_kernel_stats.csv summaries -- for the engine's kernels (lsec::)
+unless --all is given.  Per grid, because one kernel name is launched at several batch sizes.
+"""
+import csv
+import sqlite3
+import sys
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    every = "--all" in sys.argv
+    db = sqlite3.connect(args[0])
+    rows = db.execute(
+        "select name, grid_x, count(*), avg(duration), min(duration), max(duration), "
+        "max(vgpr_count + accum_vgpr_count), max(sgpr_count) from kernels group by name, grid_x "
+        "order by sum(duration) desc").fetchall()
+    out = open(args[1], "w", newline="") if len(args) > 1 else sys.stdout
+    w = csv.writer(out, quoting=csv.QUOTE_MINIMAL)
+    w.writerow(["Name", "GridX", "Calls", "AverageNs", "MinNs", "MaxNs", "VGPRs", "SGPRs"])
+    for r in rows:
+        if every or "lsec::" in r[0]:
+            w.writerow([r[0], r[1], r[2], round(r[3], 1), r[4], r[5], r[6], r[7]])
+
+
+if __name__ == "__main__":
+    main()
