@@ -292,6 +292,12 @@ int ensure_coding(PlanExt *e) {
 void host_cells(const lsec::gf8::Mat &mat, int rows, int cols, std::vector<CoefCell> &cells) {
   cells.resize(static_cast<size_t>(rows) * cols);
   for (int i = 0; i < rows * cols; ++i) lsec::make_cell(mat[i], cells[i]);
+  // flag plain-XOR rows (any launch whose first row is one takes the XOR-row kernel path)
+  for (int r = 0; r < rows; ++r) {
+    bool ones = true;
+    for (int j = 0; j < cols && ones; ++j) ones = mat[static_cast<size_t>(r) * cols + j] == 1;
+    if (ones) cells[static_cast<size_t>(r) * cols].pad |= lsec::kCellXorRow;
+  }
 }
 
 int upload_cells(const std::vector<CoefCell> &h, CoefCell **out) {

@@ -33,9 +33,11 @@ struct ShardRef {
 // wave fetches it with one scalar load.  For bytewise kernels the three 8-entry
 // product tables implement  c*v = Ta[v & 7] ^ Tb[(v >> 3) & 7] ^ Tc[v >> 6]  with one
 // v_perm_b32 each (v_perm selects bytes from an 8-byte table).
+constexpr uint32_t kCellXorRow = 1;  // CoefCell::pad of a row's first cell: every coefficient of the row is 1
+
 struct CoefCell {
   uint32_t coef;        // A[r][j] (0..255)
-  uint32_t pad;
+  uint32_t pad;         // flags (kCellXorRow in the first cell of a row)
   uint32_t ta_lo, ta_hi;  // c * {0..7}
   uint32_t tb_lo, tb_hi;  // c * {0,8,..,56}
   uint32_t tc_lo, tc_hi;  // c * {0,64,128,192}, upper 4 bytes unused

@@ -37,15 +37,17 @@ hipError_t by_r(int R, F f) {
 }
 
 // Launch shape for a K x R bytewise launch (codes in ec_kernels_impl.h).  variant 0 = the
-// automatic policy measured with tools/kbench.py (profiles/r01_v6_kbench_branchfree.txt):
+// automatic policy measured with tools/kbench.py (profiles/r01_v6_kbench_branchfree.txt,
+// r01_v10_kbench_xorrow.txt):
 //   R == 1 (single-erasure decode: XOR-heavy, read-bound)  8 B per lane, branchy cells
+//   K >= 16 (VALU-bound wide codes)                          16 B per lane, branch-free: 2 x 16 B
+//                                                            needs 256 VGPRs there (1 wave/SIMD);
+//                                                            RS 20+6 67 %, 16+4 79 % vs 51 / 63 %
 //   otherwise                                                2 x 16 B per lane, branch-free
-//                                                            (RS 20+6 encode 52 -> 62 %,
-//                                                            8+4 / 10+4 +3 points)
 int bytewise_shape(int K, int R) {
-  (void)K;
   if (g_bw_variant > 0) return (g_bw_variant - 1) % kBwShapes;
-  return R == 1 ? 4 : 0;
+  if (R == 1) return 4;
+  return K >= 16 ? 1 : 0;
 }
 
 }  // namespace

@@ -168,7 +168,12 @@ __device__ __forceinline__ void bw_fields(const typename VecT<VW>::type (&v)[IT]
   }
 }
 
-template <int R, int IT, int VW, bool TWO>
+//
+// X0: output row 0 is the plain XOR of the inputs (every coefficient 1 -- P0 of RS / Cauchy
+// encodes, and decode rows that re-encode P0), flagged by the host in the row's first cell.
+// That row then costs one 3-input XOR per input pair instead of 6 perms + 3 XORs, which
+// is what the VALU-bound wide codes pay for it otherwise (RS 20+6: 20 of 120 cells).
+template <int R, int IT, int VW, bool TWO, bool X0 = false>
 __device__ __forceinline__ void bw_accumulate_bf(typename VecT<VW>::type (&acc)[IT][R],
                                                  const typename VecT<VW>::type (&va)[IT],
                                                  const typename VecT<VW>::type (&vb)[IT], ConstCell *cells, int K, int j) {
@@ -178,6 +183,15 @@ __device__ __forceinline__ void bw_accumulate_bf(typename VecT<VW>::type (&acc)[
   if constexpr (TWO) bw_fields<IT, VW>(vb, ja, jb, jc);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
+    if constexpr (X0) {
+      if (r == 0) {
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+#pragma unroll
+          for (int e = 0; e < VW; ++e) acc[it][0][e] = TWO ? xor3(acc[it][0][e], va[it][e], vb[it][e]) : acc[it][0][e] ^ va[it][e];
+        continue;
+      }
+    }
     ConstCell *ca = cells + r * K + j;  // wave-uniform -> scalar loads
     const uint32_t a0 = ca->ta_lo, a1 = ca->ta_hi, a2 = ca->tb_lo, a3 = ca->tb_hi, a4 = ca->tc_lo;
     uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0, b4 = 0;
@@ -209,10 +223,10 @@ __device__ __forceinline__ void bw_accumulate_bf(typename VecT<VW>::type (&acc)[
 }
 
 // one input (BF = false: branchy per-cell path; true: branch-free)
-template <int R, int IT, int VW, bool BF>
+template <int R, int IT, int VW, bool BF, bool X0>
 __device__ __forceinline__ void bw_acc1(typename VecT<VW>::type (&acc)[IT][R], const typename VecT<VW>::type (&v)[IT],
                                        ConstCell *cells, int K, int j) {
-  if constexpr (BF) bw_accumulate_bf<R, IT, VW, false>(acc, v, v, cells, K, j);
+  if constexpr (BF) bw_accumulate_bf<R, IT, VW, false, X0>(acc, v, v, cells, K, j);
   else bw_accumulate<R, IT, VW>(acc, v, cells, K, j);
 }
 
@@ -253,8 +267,9 @@ __device__ __forceinline__ void magic_commit(unsigned long long *acc, uint32_t s
 
 // BF = branch-free coefficient path (bw_accumulate_bf).
 // MG = also accumulate the stripe magic of inputs + outputs (encode + je_cksum_calc fused).
-template <int R, int KC, int IT, bool BF, int VW, bool MG = false>
-__global__ __launch_bounds__(kBlock) void k_gf8_bytewise(ApplyArgs a) {
+// X0 = row 0 is a plain XOR (see bw_accumulate_bf).
+template <int R, int KC, int IT, bool BF, int VW, bool MG, bool X0>
+__device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
   typedef typename VecT<VW>::type V;
   __shared__ uint32_t red[MG ? kBlock / 64 : 1];
   constexpr int kStep = BwTile<IT, VW>::kStep;
@@ -290,8 +305,8 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bytewise(ApplyArgs a) {
         }
         if constexpr (BF) {
 #pragma unroll
-          for (int j = 0; j + 1 < KC; j += 2) bw_accumulate_bf<R, IT, VW, true>(acc, v[j], v[j + 1], cells, K, j);
-          if constexpr (KC % 2) bw_accumulate_bf<R, IT, VW, false>(acc, v[KC - 1], v[KC - 1], cells, K, KC - 1);
+          for (int j = 0; j + 1 < KC; j += 2) bw_accumulate_bf<R, IT, VW, true, X0>(acc, v[j], v[j + 1], cells, K, j);
+          if constexpr (KC % 2) bw_accumulate_bf<R, IT, VW, false, X0>(acc, v[KC - 1], v[KC - 1], cells, K, KC - 1);
         } else {
 #pragma unroll
           for (int j = 0; j < KC; ++j) bw_accumulate<R, IT, VW>(acc, v[j], cells, K, j);
@@ -310,9 +325,9 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bytewise(ApplyArgs a) {
             }
           }
           if constexpr (BF) {
-            if (nj >= 2) bw_accumulate_bf<R, IT, VW, true>(acc, v[0], v[1], cells, K, j0);
-            if (nj == 4) bw_accumulate_bf<R, IT, VW, true>(acc, v[2], v[3], cells, K, j0 + 2);
-            if (nj == 1 || nj == 3) bw_accumulate_bf<R, IT, VW, false>(acc, v[nj - 1], v[nj - 1], cells, K, j0 + nj - 1);
+            if (nj >= 2) bw_accumulate_bf<R, IT, VW, true, X0>(acc, v[0], v[1], cells, K, j0);
+            if (nj == 4) bw_accumulate_bf<R, IT, VW, true, X0>(acc, v[2], v[3], cells, K, j0 + 2);
+            if (nj == 1 || nj == 3) bw_accumulate_bf<R, IT, VW, false, X0>(acc, v[nj - 1], v[nj - 1], cells, K, j0 + nj - 1);
           } else {
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj)
@@ -344,7 +359,7 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bytewise(ApplyArgs a) {
             v[it][1] = h.y;
           }
         }
-        bw_acc1<R, IT, VW, BF>(acc, v, cells, K, j);
+        bw_acc1<R, IT, VW, BF, X0>(acc, v, cells, K, j);
         if constexpr (MG) {
           const V(*vv)[IT] = &v;
           bw_magic<R, IT, VW>(a, s, off0, K, vv, 1, j, mas, mbs);
@@ -372,6 +387,21 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bytewise(ApplyArgs a) {
       magic_commit(a.magic_acc, s, mas, mbs, red);
     }
   }
+}
+
+// The XOR-row flag (CoefCell::pad bit 0 of the launch's first cell) picks one of two whole
+// instantiations once per wave: a uniform branch outside the tile loop, no merges inside it.
+// Only codes with K*R >= 40 cells take the dual form: narrow codes are HBM-bound, and the
+// second path would only raise the kernel's register allocation (RS 6+3: 56 -> 108 VGPRs).
+template <int R, int KC, int IT, bool BF, int VW, bool MG = false>
+__global__ __launch_bounds__(kBlock) void k_gf8_bytewise(ApplyArgs a) {
+  if constexpr (BF && R >= 2 && (KC == 0 || KC * R >= 40)) {
+    if (const_cells(a.cells)->pad & kCellXorRow) {
+      bytewise_tiles<R, KC, IT, BF, VW, MG, true>(a);
+      return;
+    }
+  }
+  bytewise_tiles<R, KC, IT, BF, VW, MG, false>(a);
 }
 
 // ------------------------------------------------------------------ bitsliced
