@@ -270,7 +270,8 @@ def main():
 
     out = None
     if rank == 0:
-        cpu = None if a.no_cpu else cpu_baseline(method, k, m, C, P, a.lost, a.cpu_seconds)
+        # the reference CPU path is timed at N=1 only (one process; at N>1 it would only delay the ranks' exit)
+        cpu = None if (a.no_cpu or world > 1) else cpu_baseline(method, k, m, C, P, a.lost, a.cpu_seconds)
         host = None
         if not a.no_host_path and world == 1:
             ns = max(8, min(256, (4 << 30) // ((k + m) * C)))
