@@ -1406,6 +1406,192 @@ void parallel_copy(std::vector<HostCopy> &jobs) {
   CopyPool::get().run(j);
 }
 
+namespace {
+
+// Two pinned buffers per device for h2d_pieces / d2h_pieces.  The mutex serialises users;
+// `pending` survives a call, so the next user waits for the last DMA out of a buffer before
+// it refills it.
+struct PinnedRing {
+  static constexpr size_t kBytes = 32u << 20;
+  std::mutex mu;
+  char *buf[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  bool pending[2] = {false, false};
+
+  static PinnedRing *for_device(int dev) {
+    static std::mutex m;
+    static std::map<int, PinnedRing *> all;  // intentionally leaked: lives until exit
+    std::lock_guard<std::mutex> lk(m);
+    PinnedRing *&r = all[dev];
+    if (!r) r = new PinnedRing();
+    return r;
+  }
+  int ready() {
+    for (int b = 0; b < 2; ++b) {
+      if (!buf[b]) HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&buf[b]), kBytes, hipHostMallocDefault));
+      if (!ev[b]) HIP_OK(hipEventCreateWithFlags(&ev[b], hipEventDisableTiming));
+    }
+    return 0;
+  }
+  int wait(int b) {
+    if (!pending[b]) return 0;
+    pending[b] = false;
+    HIP_OK(hipEventSynchronize(ev[b]));
+    return 0;
+  }
+};
+
+PinnedRing *ring_here() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  return PinnedRing::for_device(dev);
+}
+
+}  // namespace
+
+int h2d_pieces(const std::vector<DevPiece> &pieces, void *stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  PinnedRing *R = ring_here();
+  if (!R) return fail("h2d_pieces: no HIP device");
+  std::lock_guard<std::mutex> lk(R->mu);
+  if (R->ready()) return -1;
+  int b = 0;
+  size_t fill = 0;
+  char *span = nullptr;  // device address of buf[b][0]
+  std::vector<CopyJob> jobs;
+  auto flush = [&]() -> int {
+    if (fill == 0) return 0;
+    CopyPool::get().run(jobs);
+    jobs.clear();
+    HIP_OK(hipMemcpyAsync(span, R->buf[b], fill, hipMemcpyHostToDevice, st));
+    HIP_OK(hipEventRecord(R->ev[b], st));
+    R->pending[b] = true;
+    b ^= 1;
+    fill = 0;
+    return 0;
+  };
+  for (const DevPiece &p : pieces) {
+    for (size_t done = 0; done < p.bytes;) {
+      if (fill > 0 && p.dev + done != span + fill && flush()) return -1;  // not contiguous on the device
+      if (fill == 0) {
+        if (R->wait(b)) return -1;
+        span = p.dev + done;
+      }
+      const size_t take = std::min(p.bytes - done, PinnedRing::kBytes - fill);
+      if (p.host)
+        jobs.push_back({R->buf[b] + fill, p.host + done, take});
+      else
+        std::memset(R->buf[b] + fill, 0, take);
+      fill += take;
+      done += take;
+      if (fill == PinnedRing::kBytes && flush()) return -1;
+    }
+  }
+  return flush();
+}
+
+static int d2h_pieces_direct(const std::vector<DevPiece> &pieces, hipStream_t st);
+
+namespace {
+
+// Scattered pieces (many small ones far apart, e.g. one rebuilt chunk per stripe of a stage)
+// are first gathered on the device into one contiguous buffer by one kernel launch; the D2H
+// then moves only useful bytes in a few large DMAs instead of one small DMA per piece.
+int d2h_gathered(const std::vector<DevPiece> &pieces, hipStream_t st) {
+  std::vector<lsec::GatherPiece> list(pieces.size());
+  size_t total = 0;
+  for (size_t i = 0; i < pieces.size(); ++i) {
+    if (pieces[i].bytes % 8 || reinterpret_cast<uintptr_t>(pieces[i].dev) % 8) return 1;  // not gatherable
+    list[i] = {reinterpret_cast<uint64_t>(pieces[i].dev), total, pieces[i].bytes};
+    total += pieces[i].bytes;
+  }
+  char *buf = nullptr;
+  HIP_OK(hipMallocAsync(reinterpret_cast<void **>(&buf), total + sizeof(lsec::GatherPiece) * list.size(), st));
+  lsec::GatherPiece *dlist = reinterpret_cast<lsec::GatherPiece *>(buf + total);  // total is a multiple of 8
+  hipError_t e = hipMemcpyAsync(dlist, list.data(), sizeof(lsec::GatherPiece) * list.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = lsec::launch_gather(dlist, static_cast<int>(list.size()), buf, st);
+  std::vector<DevPiece> packed(pieces.size());
+  for (size_t i = 0; i < pieces.size(); ++i) packed[i] = {buf + list[i].dst_off, pieces[i].host, pieces[i].bytes};
+  int rc = e == hipSuccess ? d2h_pieces_direct(packed, st) : fail("gather: %s", hipGetErrorString(e));
+  (void)hipFreeAsync(buf, st);
+  return rc;
+}
+
+}  // namespace
+
+int d2h_pieces(const std::vector<DevPiece> &pieces, void *stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // far-apart small pieces: gather on the device first (a DMA per piece costs ~40 us)
+  size_t small = 0;
+  for (size_t i = 1; i < pieces.size(); ++i)
+    small += pieces[i].dev != pieces[i - 1].dev + pieces[i - 1].bytes && pieces[i].bytes < (4u << 20);
+  if (small >= 4) {
+    const int rc = d2h_gathered(pieces, st);
+    if (rc <= 0) return rc;  // 1: not gatherable, fall through to per-window DMAs
+  }
+  return d2h_pieces_direct(pieces, st);
+}
+
+static int d2h_pieces_direct(const std::vector<DevPiece> &pieces, hipStream_t st) {
+  PinnedRing *R = ring_here();
+  if (!R) return fail("d2h_pieces: no HIP device");
+  // windows: device ranges of at most one ring buffer, covering runs of pieces whose gaps are
+  // small (a gap is transferred and discarded: cheaper than another DMA below ~1 MiB)
+  struct Window {
+    char *dev;
+    size_t len;
+    char *alloc_end;           // a window never crosses the end of the allocation it starts in
+    std::vector<CopyJob> out;  // src = offset into the window (fixed up at unpack time)
+  };
+  constexpr size_t kGap = 1u << 20;
+  std::vector<Window> win;
+  char *abase = nullptr, *aend = nullptr;  // allocation of the last piece looked up
+  for (const DevPiece &p : pieces)
+    for (size_t done = 0; done < p.bytes;) {
+      char *d = p.dev + done;
+      const size_t take = std::min(p.bytes - done, PinnedRing::kBytes);
+      if (!(d >= abase && d < aend)) {
+        hipDeviceptr_t b = nullptr;
+        size_t sz = 0;
+        if (hipMemGetAddressRange(&b, &sz, d) != hipSuccess) {
+          (void)hipGetLastError();
+          b = d;  // unknown extent: no gap merging past this piece
+          sz = p.bytes - done;
+        }
+        abase = static_cast<char *>(b);
+        aend = abase + sz;
+      }
+      const bool fits = !win.empty() && d >= win.back().dev + win.back().len && d <= win.back().dev + win.back().len + kGap &&
+                        d + take <= win.back().alloc_end && d >= abase && win.back().dev >= abase &&
+                        static_cast<size_t>(d + take - win.back().dev) <= PinnedRing::kBytes;
+      if (!fits) win.push_back({d, 0, aend, {}});
+      Window &w = win.back();
+      w.out.push_back({p.host + done, reinterpret_cast<const char *>(d - w.dev), take});
+      w.len = static_cast<size_t>(d + take - w.dev);
+      done += take;
+    }
+  std::lock_guard<std::mutex> lk(R->mu);
+  if (R->ready()) return -1;
+  auto unpack = [&](size_t i) -> int {
+    const int b = static_cast<int>(i & 1);
+    if (R->wait(b)) return -1;
+    for (CopyJob &j : win[i].out) j.src = R->buf[b] + reinterpret_cast<uintptr_t>(j.src);
+    CopyPool::get().run(win[i].out);
+    return 0;
+  };
+  for (size_t i = 0; i < win.size(); ++i) {
+    const int b = static_cast<int>(i & 1);
+    if (i >= 2 && unpack(i - 2)) return -1;  // frees buffer b
+    if (R->wait(b)) return -1;
+    HIP_OK(hipMemcpyAsync(R->buf[b], win[i].dev, win[i].len, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipEventRecord(R->ev[b], st));
+    R->pending[b] = true;
+  }
+  for (size_t i = win.size() >= 2 ? win.size() - 2 : 0; i < win.size(); ++i)
+    if (unpack(i)) return -1;
+  return 0;
+}
+
 void make_word_cell(uint32_t c, int w, uint32_t *out) {
   for (int b = 0; b < w; ++b, c = gfw::times_x(c, w)) out[b] = (w == 16) ? (c | (c << 16)) : c;
 }

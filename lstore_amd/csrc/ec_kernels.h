@@ -97,6 +97,16 @@ struct DiffArgs {
 };
 hipError_t launch_chunk_diff(const DiffArgs &a, hipStream_t stream);
 
+// Device-side gather of scattered byte ranges into one contiguous buffer (so a scattered
+// device -> host transfer becomes one DMA): dst + dst_off[i] <- src[i], bytes[i] (multiples of
+// 8, 8-byte aligned).  `list` is in device memory; one block per piece.
+struct GatherPiece {
+  uint64_t src;
+  uint64_t dst_off;
+  uint64_t bytes;
+};
+hipError_t launch_gather(const GatherPiece *list, int n, char *dst, hipStream_t stream);
+
 // Host helper: fill one cell for coefficient c.
 void make_cell(uint8_t c, CoefCell &cell);
 

@@ -210,7 +210,20 @@ __global__ __launch_bounds__(kBlock) void k_chunk_diff(DiffArgs a) {
   }
 }
 
+__global__ __launch_bounds__(kBlock) void k_gather(const GatherPiece *list, char *dst) {
+  const GatherPiece g = list[blockIdx.x];
+  const LSEC_GLOBAL u32x2 *src = gptr<u32x2>(g.src);
+  LSEC_GLOBAL u32x2 *out = gptr_w<u32x2>(reinterpret_cast<uint64_t>(dst) + g.dst_off);
+  for (uint64_t i = threadIdx.x; i < g.bytes / 8; i += kBlock) out[i] = __builtin_nontemporal_load(src + i);
+}
+
 }  // namespace
+
+hipError_t launch_gather(const GatherPiece *list, int n, char *dst, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather, dim3(n), dim3(kBlock), 0, st, list, dst);
+  return hipGetLastError();
+}
 
 hipError_t launch_chunk_diff(const DiffArgs &a, hipStream_t st) {
   if (a.npairs < 1 || a.npairs > kMaxR || a.size % 8 != 0 || !a.flags) return hipErrorInvalidValue;

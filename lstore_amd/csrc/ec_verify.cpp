@@ -29,6 +29,9 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
+#include <cstdio>
+#include <string>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -52,6 +55,29 @@ size_t verify_budget() {
   return b;
 }
 
+// LSEC_TRACE=1: per-phase wall times of a read / inspection on stderr (synchronises the
+// stage stream at each mark, so the times add up).
+struct Trace {
+  const char *what;
+  hipStream_t st = nullptr;
+  bool on = getenv("LSEC_TRACE") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  std::string line;
+  explicit Trace(const char *w) : what(w) {}
+  void mark(const char *phase) {
+    if (!on) return;
+    if (st) (void)hipStreamSynchronize(st);
+    const auto now = std::chrono::steady_clock::now();
+    char buf[96];
+    snprintf(buf, sizeof(buf), " %s %.2f ms", phase, std::chrono::duration<double, std::milli>(now - t).count());
+    line += buf;
+    t = now;
+  }
+  ~Trace() {
+    if (on) fprintf(stderr, "lsec trace %s:%s\n", what, line.c_str());
+  }
+};
+
 // W stripes of n logical chunks in HBM ([W][n][C]) plus m rebuild slots per stripe
 struct Stage {
   int W = 0, n = 0, m = 0;
@@ -67,11 +93,14 @@ struct Stage {
   Stage(const Stage &) = delete;
   Stage &operator=(const Stage &) = delete;
   ~Stage() { release(); }
+  // Stream-ordered allocations from the device's memory pool: a verification pass allocates
+  // and frees a stage per bad-set group, and hipMalloc / hipFree (a device-wide sync) per
+  // group cost more than the group's work.  See keep_pool().
   void release() {
-    if (d) (void)hipFree(d);
-    if (slots) (void)hipFree(slots);
-    if (dmag) (void)hipFree(dmag);
-    if (dflag) (void)hipFree(dflag);
+    if (d) (void)hipFreeAsync(d, st);
+    if (slots) (void)hipFreeAsync(slots, st);
+    if (dmag) (void)hipFreeAsync(dmag, st);
+    if (dflag) (void)hipFreeAsync(dflag, st);
     d = slots = nullptr;
     dmag = nullptr;
     dflag = nullptr;
@@ -80,9 +109,10 @@ struct Stage {
     release();
     W = W_, n = n_, m = m_, C = C_, st = s;
     if (W == 0) return 0;
-    if (hipMalloc(&d, static_cast<size_t>(W) * n * C) != hipSuccess ||
-        hipMalloc(&slots, static_cast<size_t>(W) * m * C) != hipSuccess ||
-        hipMalloc(&dmag, static_cast<size_t>(W) * 4) != hipSuccess || hipMalloc(&dflag, sizeof(int) * W) != hipSuccess)
+    if (hipMallocAsync(reinterpret_cast<void **>(&d), static_cast<size_t>(W) * n * C, st) != hipSuccess ||
+        hipMallocAsync(reinterpret_cast<void **>(&slots), static_cast<size_t>(W) * m * C, st) != hipSuccess ||
+        hipMallocAsync(reinterpret_cast<void **>(&dmag), static_cast<size_t>(W) * 4, st) != hipSuccess ||
+        hipMallocAsync(reinterpret_cast<void **>(&dflag), sizeof(int) * W, st) != hipSuccess)
       return -1;
     hmag.assign(static_cast<size_t>(W) * 4, 0);
     hflag.assign(W, 0);
@@ -242,21 +272,27 @@ struct Repair {
   uint8_t magic[4] = {0, 0, 0, 0};
 };
 
-int capture(const Stage &S, int w, const Check &ck, const std::vector<int> &bad, Repair &rp, bool full = false) {
+// Queue the device->host copies that capture a passed check for stripe w of S into rp (the
+// rebuilt devices, and with `full` every chunk as eptr holds it); one d2h_pieces call then
+// moves a whole batch of stripes.  rp's buffers must stay put until that call.
+void capture_q(const Stage &S, int w, const Check &ck, const std::vector<int> &bad, Repair &rp, bool full,
+               std::vector<lsec::DevPiece> &q) {
   rp.ok = true;
   rp.bad = bad;
   rp.rebuilt.resize(bad.size() * S.C);
-  for (size_t i = 0; i < bad.size(); ++i)
-    if (hipMemcpy(&rp.rebuilt[i * S.C], S.slot(w, ck.slot_of[bad[i]]), S.C, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  for (size_t i = 0; i < bad.size(); ++i) q.push_back({S.slot(w, ck.slot_of[bad[i]]), &rp.rebuilt[i * S.C], S.C});
   std::memcpy(rp.magic, &S.hmag[static_cast<size_t>(w) * 4], 4);
   if (full) {
     rp.full.resize(static_cast<size_t>(S.n) * S.C);
-    for (int j = 0; j < S.n; ++j) {
-      const char *src = ck.slot_of[j] >= 0 ? S.slot(w, ck.slot_of[j]) : S.chunk(w, j);
-      if (hipMemcpy(&rp.full[static_cast<size_t>(j) * S.C], src, S.C, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    }
+    for (int j = 0; j < S.n; ++j)
+      q.push_back({ck.slot_of[j] >= 0 ? S.slot(w, ck.slot_of[j]) : S.chunk(w, j), &rp.full[static_cast<size_t>(j) * S.C], S.C});
   }
-  return 0;
+}
+
+int capture(const Stage &S, int w, const Check &ck, const std::vector<int> &bad, Repair &rp, bool full = false) {
+  std::vector<lsec::DevPiece> q;
+  capture_q(S, w, ck, bad, rp, full, q);
+  return lsec::d2h_pieces(q, S.st);
 }
 
 // the stripe buffer of an unresolved stripe (with the in-place rebuilds of its failed checks)
@@ -292,15 +328,16 @@ int brute_enumerate(lio_erasure_plan_t *plan, Stage &F, const std::vector<Magic>
       Check ck;
       if (control_check(plan, *cur, 0, cur->W, combo, cksum ? mg.data() : nullptr, want_magic, ck) != 0) return -1;
       std::vector<int> still;
+      std::vector<lsec::DevPiece> q;
       for (int i = 0; i < cur->W; ++i) {
         const int t = cur_ids[i];
         if (!std::binary_search(rem.begin(), rem.end(), t)) continue;
-        if (ck.pass[i]) {
-          if (capture(*cur, i, ck, combo, out[t], true) != 0) return -1;
-        } else {
+        if (ck.pass[i])
+          capture_q(*cur, i, ck, combo, out[t], true, q);
+        else
           still.push_back(t);
-        }
       }
+      if (lsec::d2h_pieces(q, cur->st) != 0) return -1;
       rem.swap(still);
       if (cur == &F && !rem.empty() && rem.size() * 2 <= static_cast<size_t>(F.W)) {
         if (gather_new(F, rem, G) != 0) return -1;
@@ -382,17 +419,22 @@ int verify_batch(lio_erasure_plan_t *plan, Stage &S, const std::vector<std::vect
   rp.assign(W, Repair());
   std::map<std::vector<int>, std::vector<int>> groups;
   for (int w = 0; w < W; ++w) groups[bad[w]].push_back(w);
-  // the most common bad set runs over the whole stage (other stripes' results are ignored);
-  // the rest are gathered
+  // A group runs over the whole stage (the other stripes' results are ignored) when that is
+  // cheaper than gathering it: it is the most common bad set, it holds at least a quarter of
+  // the stage, or the stage is small (<= 1 GiB: a full decode + magic pass is ~0.3 ms of HBM
+  // time, less than the launches of a per-stripe gather).  Smaller groups are gathered.
   auto big = std::max_element(groups.begin(), groups.end(),
                               [](const auto &a, const auto &b) { return a.second.size() < b.second.size(); });
+  const bool small_stage = static_cast<size_t>(W) * (S.n + S.m) * S.C <= (1ull << 30);
+  Trace tr("verify_batch");
+  tr.st = S.st;
   std::vector<char> fail(W, 0);
   for (auto it = groups.begin(); it != groups.end(); ++it) {
     Stage G;
     Stage *T = &S;
     std::vector<int> ids;  // S index of each stripe of *T
     InPlace ip{&S, {}};
-    if (it == big) {
+    if (it == big || small_stage || it->second.size() * 4 >= static_cast<size_t>(W)) {
       for (int w = 0; w < W; ++w) {
         ids.push_back(w);
         ip.at.push_back(bad[w] == it->first ? w : -1);
@@ -405,14 +447,19 @@ int verify_batch(lio_erasure_plan_t *plan, Stage &S, const std::vector<std::vect
     }
     const std::vector<uint8_t> tm = flat(mg, ids);
     Check ck;
+    tr.mark("group");
     if (control_check(plan, *T, 0, static_cast<int>(ids.size()), it->first, cksum ? tm.data() : nullptr, want_magic, ck, &ip) != 0)
       return -1;
+    tr.mark("check");
+    std::vector<lsec::DevPiece> q;
     for (size_t i = 0; i < ids.size(); ++i) {
       const int w = ids[i];
       if (bad[w] != it->first) continue;
       if (!ck.pass[i]) fail[w] = 1;
-      else if ((!it->first.empty() || want_magic) && capture(*T, static_cast<int>(i), ck, it->first, rp[w]) != 0) return -1;
+      else if (!it->first.empty() || want_magic) capture_q(*T, static_cast<int>(i), ck, it->first, rp[w], false, q);
     }
+    if (lsec::d2h_pieces(q, T->st) != 0) return -1;
+    tr.mark("capture");
   }
   std::vector<int> failing;
   for (int w = 0; w < W; ++w)
@@ -480,6 +527,19 @@ bool all_zero(const char *p, size_t C) {
   return true;
 }
 
+// Keep up to two verification budgets of freed stage memory in the current device's default
+// pool between calls (the default release threshold of 0 hands it back at every sync).
+void keep_pool() {
+  int dev = 0;
+  hipMemPool_t pool = nullptr;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  uint64_t keep = 2 * verify_budget();
+  if (hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess) (void)hipGetLastError();
+}
+
 int stripes_per_batch(int n, int m, size_t C) {
   return static_cast<int>(std::max<size_t>(1, verify_budget() / ((static_cast<size_t>(n) + m) * C)));
 }
@@ -496,6 +556,7 @@ int lsec_segment_read(lio_erasure_plan_t *plan, char **dev, int nstripes, int ch
   const size_t C = static_cast<size_t>(chunk), lchunk = C + 4;
   const bool paranoid = flags & LSEC_READ_PARANOID, cksum = !(flags & LSEC_MAGIC_LEGACY);
   if (nstripes == 0) return 0;
+  Trace tr("read");
   // logical chunk j of stripe s lives on device (j - ss*n_shift) mod n  (lun.c:1178-1223)
   auto phys = [&](long long ss, int j) { return static_cast<int>(((j - ss * n_shift) % n + n) % n); };
   auto rec = [&](int s, int j) -> const char * {  // [magic | chunk] record, nullptr if unreadable
@@ -542,9 +603,12 @@ int lsec_segment_read(lio_erasure_plan_t *plan, char **dev, int nstripes, int ch
   }
 
   // ---- 2. verification / repair on the GPU, in stripe order, budget-sized batches
+  tr.mark("classify");
   std::vector<Repair> repair(nstripes);
   hipStream_t stream = nullptr;
+  if (!work.empty()) keep_pool();
   if (!work.empty() && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return -1;
+  tr.st = stream;
   BruteState bs;
   int rc = 0;
   const int wmax = stripes_per_batch(n, m, C);
@@ -554,20 +618,23 @@ int lsec_segment_read(lio_erasure_plan_t *plan, char **dev, int nstripes, int ch
     if (S.alloc(W, n, m, C, stream) != 0) { rc = -1; break; }
     std::vector<std::vector<int>> bad(W);
     std::vector<Magic> mg(W);
-    for (int w = 0; w < W && rc == 0; ++w) {
+    std::vector<lsec::DevPiece> pieces;  // chunks in staging order; unreadable devices stage zeros
+    pieces.reserve(static_cast<size_t>(W) * n);
+    for (int w = 0; w < W; ++w) {
       const int s = work[b0 + w];
       bad[w] = q[s].bad;
       mg[w] = q[s].magic;
       for (int j = 0; j < n; ++j) {
         const char *p = rec(s, j);
-        const hipError_t e = p ? hipMemcpyAsync(S.chunk(w, j), p + 4, C, hipMemcpyHostToDevice, stream)
-                               : hipMemsetAsync(S.chunk(w, j), 0, C, stream);
-        if (e != hipSuccess) rc = -1;
+        pieces.push_back({S.chunk(w, j), p ? const_cast<char *>(p) + 4 : nullptr, C});
       }
     }
+    if (lsec::h2d_pieces(pieces, stream) != 0) rc = -1;
+    tr.mark("stage");
     std::vector<int> res;
     std::vector<Repair> rp;
     if (rc || verify_batch(plan, S, bad, mg, cksum, false, bs, res, rp) != 0) { rc = -1; break; }
+    tr.mark("verify");
     for (int w = 0; w < W; ++w) {
       const int s = work[b0 + w];
       if (res[w] < 0) st[s] = kLost;
@@ -575,6 +642,7 @@ int lsec_segment_read(lio_erasure_plan_t *plan, char **dev, int nstripes, int ch
       repair[s] = std::move(rp[w]);
     }
   }
+  tr.st = nullptr;
   if (stream) (void)hipStreamDestroy(stream);
   if (rc) return -1;
 
@@ -602,6 +670,7 @@ int lsec_segment_read(lio_erasure_plan_t *plan, char **dev, int nstripes, int ch
     }
   }
   lsec::parallel_copy(jobs);
+  tr.mark("copyout");
   return unrecoverable;
 }
 
@@ -651,6 +720,7 @@ int lsec_segment_inspect(lio_erasure_plan_t *plan, char *buf, int nstripes, int 
   std::vector<std::vector<int>> final_bad(nstripes);
   for (int s = 0; s < nstripes; ++s) final_bad[s] = q[s].bad;
   hipStream_t stream = nullptr;
+  if (!work.empty()) keep_pool();
   if (!work.empty() && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return -1;
   const int wmax = stripes_per_batch(n, m, C);
   int rc = 0;
@@ -658,15 +728,12 @@ int lsec_segment_inspect(lio_erasure_plan_t *plan, char *buf, int nstripes, int 
     const int W = static_cast<int>(std::min<size_t>(wmax, work.size() - b0));
     Stage S;
     if (S.alloc(W, n, m, C, stream) != 0) { rc = -1; break; }
-    // stage: one strided copy per contiguous run of stripes ([magic | chunk] -> chunk)
-    for (int w = 0; w < W && rc == 0;) {
-      int e = w + 1;
-      while (e < W && work[b0 + e] == work[b0 + e - 1] + 1) ++e;
-      if (hipMemcpy2DAsync(S.chunk(w, 0), C, rec(work[b0 + w], 0) + 4, lchunk, C, static_cast<size_t>(e - w) * n,
-                           hipMemcpyHostToDevice, stream) != hipSuccess)
-        rc = -1;
-      w = e;
-    }
+    // stage the chunks ([magic | chunk] records -> chunks), packed into large DMAs
+    std::vector<lsec::DevPiece> pieces;
+    pieces.reserve(static_cast<size_t>(W) * n);
+    for (int w = 0; w < W; ++w)
+      for (int j = 0; j < n; ++j) pieces.push_back({S.chunk(w, j), rec(work[b0 + w], j) + 4, C});
+    if (lsec::h2d_pieces(pieces, stream) != 0) rc = -1;
     std::vector<std::vector<int>> bad(W);
     std::vector<Magic> mg(W);
     for (int w = 0; w < W; ++w) {

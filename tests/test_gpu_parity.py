@@ -237,6 +237,43 @@ def test_ragged_chunk_sizes_bytewise(cuda, size):
         assert np.array_equal(sh, full)
 
 
+@pytest.mark.parametrize("method,k,m,size", [
+    (L.REED_SOL_VAN, 16, 4, 65536 + 4104),    # K >= 16: 16 B/lane shape + XOR-row path, ragged last tile
+    (L.REED_SOL_VAN, 20, 6, 3 * 4096 + 8),
+    (L.REED_SOL_VAN, 17, 5, 40960 + 16),      # generic-K kernel (KC = 0) with the XOR-row path
+    (L.REED_SOL_VAN, 12, 10, 24576),          # R = 10 > 8: two launches (rows 0-7 with the XOR row, 8-9)
+    (L.REED_SOL_R6_OP, 20, 2, 32768 + 24),    # r6: P row all ones
+    (L.CAUCHY_ORIG, 10, 4, 8192),             # bitsliced (no all-ones row): unaffected control
+])
+def test_xor_row_and_wide_shapes_vs_oracle(cuda, method, k, m, size):
+    """Kernel paths chosen by code width: wide codes (16 B/lane), the plain-XOR first row (all-ones
+    coefficients) and launches split at 8 rows -- encode and decodes whose first decode row is
+    all ones (P0 lost with data) or not, bit-exact vs the oracle."""
+    import torch
+
+    n = 3
+    P = 128 if method == L.CAUCHY_ORIG else 0
+    st = np.zeros((n, k + m, size), dtype=np.uint8)
+    st[:, :k] = np.random.default_rng(k * 7 + m).integers(0, 256, (n, k, size), dtype=np.uint8)
+    with L.Plan.new(method, size, k, m, 8, P or 8, 8) as p:
+        assert p.form_encoding_matrix() == 0 and p.form_decoding_matrix() == 0
+        d = torch.from_numpy(st[:, :k].copy()).to(cuda)
+        par = torch.zeros((n, m, size), dtype=torch.uint8, device=cuda)
+        p.encode_dev(d, par)
+        torch.cuda.synchronize()
+        hp = par.cpu().numpy()
+        for s in range(n):
+            assert np.array_equal(hp[s], O.encode(method, st[s, :k], m, P)), s
+        full = np.concatenate([st[:, :k], hp], axis=1)
+        for pat in ([k], [0, k], [1, k, k + m - 1], [0], list(range(min(m, 3)))):
+            if len(pat) > m:
+                continue
+            sh = full.copy()
+            sh[:, pat] = 0x77
+            p.decode_stripes(sh, pat)
+            assert np.array_equal(sh, full), pat
+
+
 @pytest.mark.parametrize("P", [8, 16, 24, 40, 4096])
 def test_bitsliced_packet_sizes(cuda, P):
     k, m = 6, 3

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""BASELINE config c1: RS(6+3) encode of 1000 x 64 KiB stripes through the segment write path.
+"""BASELINE config c1: RS(6+3) encode of 1000 x 64 KiB stripes through the segment write path,
+and the segment read / inspection paths over the images it wrote.
 
 The reference's c1 runs src/lio over vendor/jerasure into loopback IBP depots.  IBP
 (APR/ZMQ/leveldb) cannot be built offline, so the depots are files:
@@ -8,6 +9,14 @@ The reference's c1 runs src/lio over vendor/jerasure into loopback IBP depots.  
   engine     lsec_segment_write: one call, parity + magic on the GPU
 Both produce k+m device images; they must be byte-identical.  Rates are user-data GiB/s,
 with and without writing the images to depot files (--depot-dir, default /tmp).
+
+Then, over the same images, reference harness vs engine:
+  read        segjerase_read_func's verification (lsec_segment_read): clean, paranoid (every
+              stripe verified), and degraded (device 0's magic stale in every stripe: quorum,
+              rebuild of one chunk per stripe, verification)
+  inspect     segjerase_inspect_full_func (lsec_segment_inspect) over the LUN records with
+              one silently corrupted byte in every 25th stripe (brute-force search)
+Outputs (user data, stripe status, bad-device maps) must be identical.
 """
 import argparse
 import json
@@ -72,6 +81,7 @@ def main():
         for i in range(k + m):
             os.remove(os.path.join(a.depot_dir, f"{tag}_depot{i}.bin"))
     tr, te = min(t_ref), min(t_eng)
+    paths = verify_paths(plan, rp, ours, N, C, k, m, a.n_shift, a.reps) if identical else {}
     print(json.dumps({
         "config": "c1", "workload": f"{a.method}({k}+{m}) segment write, {N} stripes x C={C} B, n_shift={a.n_shift}",
         "images_identical": identical,
@@ -82,9 +92,51 @@ def main():
         "depot_dir": a.depot_dir,
         "note": "reference = segjerase_write_func loop over real jerasure + zlib (oracle/_ref); engine = "
                 "lsec_segment_write (GPU parity + magic, host memory in/out, PCIe included)",
+        "read_inspect": paths,
     }), flush=True)
-    if not identical:
+    if not identical or not all(v.get("identical") for v in paths.values()):
         sys.exit(1)
+
+
+def timed(fn, reps):
+    best, out = None, None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = fn()
+        t = time.perf_counter() - t0
+        best = t if best is None else min(best, t)
+    return best, out
+
+
+def verify_paths(plan, rp, img, N, C, k, m, n_shift, reps):
+    """Read (clean / paranoid / degraded) and inspection: reference harness vs engine."""
+    n, lc = k + m, C + 4
+    gib = k * C * N / 2**30
+    res = {}
+    degraded = img.copy()
+    degraded[0].reshape(N, lc)[:, 0] ^= 0x11          # device 0: stale magic in every stripe
+    for name, im, par in (("read_clean", img, 0), ("read_paranoid", img, 1), ("read_degraded", degraded, 0)):
+        tr, (rout, rst, rbad) = timed(lambda: rp.segment_read(im, N, C, n_shift, 0, par, 1), reps)
+        te, (out, st, bad) = timed(lambda: plan.segment_read(im, N, C, n_shift, 0, paranoid=bool(par)), reps)
+        res[name] = {"identical": bool(np.array_equal(out, rout) and np.array_equal(st, rst) and bad == rbad),
+                     "reference_cpu_gibps": round(gib / tr, 3), "engine_gibps": round(gib / te, 3),
+                     "stripes_recovered": int((st == 1).sum())}
+    # LUN records [N][n][C+4] (device d holds logical chunk (d + s*n_shift) % n of stripe s)
+    rec = np.empty((N, n, lc), np.uint8)
+    for d in range(n):
+        rows = img[d].reshape(N, lc)
+        for s in range(N):
+            rec[s, (d + s * n_shift) % n] = rows[s]
+    rng = np.random.default_rng(25)
+    for s in range(0, N, 25):                         # silent corruption: one byte of one chunk
+        rec[s, int(rng.integers(0, n)), 4 + int(rng.integers(0, C))] ^= 0x5A
+    tr, (rst, rbm, _, rcnt, _) = timed(lambda: rp.segment_inspect(rec.copy(), N, C, 1, 0), reps)
+    te, (st, bm, _, state) = timed(lambda: plan.segment_inspect(rec.copy(), C), reps)
+    res["inspect"] = {"identical": bool(np.array_equal(st, rst) and np.array_equal(bm, rbm) and
+                                        state.bad_stripes == rcnt[0] and state.silent_errors == rcnt[2]),
+                      "reference_cpu_gibps": round(gib / tr, 3), "engine_gibps": round(gib / te, 3),
+                      "stripes_repaired": int((st == 3).sum())}
+    return res
 
 
 if __name__ == "__main__":
