@@ -1950,12 +1950,14 @@ int lsec_encode_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, 
   if (!shards || !magic) return fail("shards / magic is NULL");
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int k = plan->data_strips, m = plan->parity_strips;
-  // One pass when the encode is light enough to absorb the magic's VALU work: the encode
-  // kernel also accumulates the magic of the k inputs and m outputs.  Past k*m = 64 the fused
-  // kernel turns VALU-bound and encode + magic as two HBM passes is faster (RS 20+6:
-  // 13.4 ms fused vs 11.7 ms; RS 16+4: 6.2 ms fused vs 10.8 ms; profiles/r01_v7_*).
-  if (kernel_kind(plan->method, plan->w) == KBYTEWISE && m <= 8 && k * m <= 64 && !check_geometry(plan, block_size) &&
-      k + m <= lsec::kMaxMagicShards) {
+  // One pass: the encode kernel also accumulates the magic of the k inputs and m outputs.
+  // Each lane keeps it in 32-bit dot-product chains (MagicLane, ec_kernels_impl.h), about
+  // 3 VALU ops per data dword, so fusing wins at every k, m a single launch takes (m <= 8):
+  // RS 12+4 5.9 ms fused vs 5.7 + 5.2 ms as two passes, Cauchy 6+3 5.9 vs 5.9 + 6.2 ms
+  // (profiles/r01_v12_kbench_fused_magic.txt).
+  const int kind = kernel_kind(plan->method, plan->w);
+  const bool fuse = kind == KBYTEWISE || kind == KBITSLICED;
+  if (fuse && m <= 8 && !check_geometry(plan, block_size) && k + m <= lsec::kMaxMagicShards) {
     if (nstripes <= 0 || block_size == 0) return 0;
     const void *cells = nullptr;
     if (encode_cells(e, &cells)) return -1;
@@ -1969,6 +1971,7 @@ int lsec_encode_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, 
     a.K = k;
     a.R = m;
     a.size = block_size;
+    a.packet = plan->packet_size;
     const int per = static_cast<int>(std::max(1LL, (1LL << 30) / std::max(1LL, block_size / 8192 + 1)));
     for (int s0 = 0; s0 < nstripes; s0 += per) {
       a.nstripes = std::min(per, nstripes - s0);
@@ -1978,7 +1981,7 @@ int lsec_encode_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, 
       for (int r = 0; r < m; ++r)
         a.out[r] = {reinterpret_cast<uint64_t>(shards[k + r].base) + static_cast<uint64_t>(s0) * shards[k + r].stride,
                     shards[k + r].stride};
-      HIP_OK(lsec::launch_bytewise_magic(a, st));
+      HIP_OK(kind == KBITSLICED ? lsec::launch_bitsliced(a, st) : lsec::launch_bytewise_magic(a, st));
     }
     HIP_OK(lsec::launch_magic_finalize(acc, nstripes, static_cast<int64_t>(k + m) * block_size,
                                        static_cast<uint8_t *>(magic), st));

@@ -53,7 +53,7 @@ struct ApplyArgs {
   const uint32_t *masks;  // bitmatrix: (R*w) x K words, bit x of [(r*w+l)*K + j] = B[r*w+l][j*w+x]
                           // wordwise: R x K x w products, [(r*K + j)*w + b] = c_rj * x^b
   int w;                  // bitmatrix: packets per super-packet; wordwise: field width (16 / 32)
-  unsigned long long *magic_acc;  // bytewise encode only: fused stripe magic over the K inputs then the
+  unsigned long long *magic_acc;  // encode only (bytewise, bitsliced): fused stripe magic over the K inputs then the
                                   // R outputs (2 x u64 per stripe, zeroed), see MagicArgs
   ShardRef in[kMaxK];
   ShardRef out[kMaxR];

@@ -71,7 +71,7 @@ hipError_t launch_bytewise(const ApplyArgs &a, hipStream_t st, int grid_blocks) 
 hipError_t launch_bytewise_magic(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
   if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > 8 || a.size % 8 != 0 || !a.magic_acc) return hipErrorInvalidValue;
   if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
-  const uint64_t tile = static_cast<uint64_t>(kBlock) * 16 * 2;
+  const uint64_t tile = static_cast<uint64_t>(kBlock) * 16 * (a.K >= 16 ? 1 : 2);  // dispatch_bytewise_magic's IT
   const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);
@@ -83,7 +83,7 @@ hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid_blocks)
       a.size % (8LL * a.packet) != 0)
     return hipErrorInvalidValue;
   if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
-  int dw = (g_bs_variant == 2 || g_bs_variant == 4) ? g_bs_variant : 1;
+  int dw = (g_bs_variant == 2 || g_bs_variant == 4) && !a.magic_acc ? g_bs_variant : 1;
   while (dw > 1 && a.packet % (4 * dw) != 0) dw >>= 1;
   const uint64_t col_bytes = a.size / 8;
   const uint64_t tile = kBlock * 4ull * dw;

@@ -230,38 +230,66 @@ __device__ __forceinline__ void bw_acc1(typename VecT<VW>::type (&acc)[IT][R], c
   else bw_accumulate<R, IT, VW>(acc, v, cells, K, j);
 }
 
-// fused stripe magic: every lane adds its bytes' position-weighted sums, the block reduces
-// them and adds one pair per tile into the stripe's accumulator
-template <int R, int IT, int VW>
-__device__ __forceinline__ void bw_magic(const ApplyArgs &a, uint32_t s, int64_t off0, int K,
-                                         const typename VecT<VW>::type (*v)[IT], int nv, int j0,
-                                         uint64_t &as, uint64_t &bs) {
-  constexpr int kStep = kBlock * 4 * VW;
-  const uint64_t L = static_cast<uint64_t>(K + R) * a.size;
-  for (int jj = 0; jj < nv; ++jj)
-#pragma unroll
-    for (int it = 0; it < IT; ++it)
-      adler_add(v[jj][it], L - static_cast<uint64_t>((j0 + jj) * a.size + off0 + it * kStep), as, bs);
-}
-
-template <int R, int IT, int VW>
-__device__ __forceinline__ void bw_magic_out(const ApplyArgs &a, int64_t off0, int K,
-                                             const typename VecT<VW>::type (&acc)[IT][R], uint64_t &as, uint64_t &bs) {
-  constexpr int kStep = kBlock * 4 * VW;
-  const uint64_t L = static_cast<uint64_t>(K + R) * a.size;
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-#pragma unroll
-    for (int it = 0; it < IT; ++it)
-      adler_add(acc[it][r], L - static_cast<uint64_t>((K + r) * a.size + off0 + it * kStep), as, bs);
-}
-
 __device__ __forceinline__ void magic_commit(unsigned long long *acc, uint32_t s, uint64_t as, uint64_t bs, uint32_t *red) {
   const uint32_t am = block_sum(static_cast<uint32_t>(as % kAdlerMod), red);
   const uint32_t bm = block_sum(static_cast<uint32_t>(bs % kAdlerMod), red);
   if (threadIdx.x == 0) {
     atomicAdd(acc + 2 * s, static_cast<unsigned long long>(am));
     atomicAdd(acc + 2 * s + 1, static_cast<unsigned long long>(bm));
+  }
+}
+
+// Per-lane partial sums of the fused stripe magic.  A lane's byte at stripe position
+//   p = sh*C + off + x*X + 4d + t
+// (shard sh, the lane's first byte `off`, its x-th word group X bytes further on -- the
+// iteration of the bytewise kernel, the packet of the bit-sliced one -- dword d, byte t)
+// contributes (L - p)*b to adler32's B, so over the lane's bytes
+//   sum (L - p) b = L*A - (C*JS + off*A + X*XS + W)
+// with A = sum b, JS = sum sh*b, XS = sum x*b, W = sum (4d+t)*b: 32-bit v_dot4 chains,
+// no 64-bit arithmetic until the lane's tile is done.
+struct MagicLane {
+  uint32_t a = 0, js = 0, xs = 0, w = 0;
+};
+
+__device__ __forceinline__ void ml_commit(const MagicLane &m, unsigned long long *acc, uint32_t s, int nsh, uint64_t C,
+                                          uint64_t off, uint64_t X, uint32_t *red) {
+  const uint64_t A = m.a;
+  const uint64_t B = static_cast<uint64_t>(nsh) * C * A - (C * m.js + off * A + X * m.xs + m.w);
+  magic_commit(acc, s, A, B, red);
+}
+
+// one shard's words of a lane: e[x] = VW dwords, x = 0..NX-1
+template <int NX, int VW>
+__device__ __forceinline__ void ml_add(MagicLane &m, const typename VecT<VW>::type (&e)[NX], uint32_t sh) {
+  uint32_t sum = 0;
+#pragma unroll
+  for (int x = 0; x < NX; ++x)
+#pragma unroll
+    for (int d = 0; d < VW; ++d) {
+      const uint32_t v = reinterpret_cast<const uint32_t *>(&e[x])[d];
+      sum = __builtin_amdgcn_udot4(v, 0x01010101u, sum, false);
+      if (NX > 1) m.xs = __builtin_amdgcn_udot4(v, 0x01010101u * x, m.xs, false);
+      m.w = __builtin_amdgcn_udot4(v, 0x03020100u + 0x04040404u * d, m.w, false);
+    }
+  m.a += sum;
+  m.js += sh * sum;
+}
+
+// fused stripe magic (bytewise kernel): lane words are the IT steps kStep bytes apart
+template <int R, int IT, int VW>
+__device__ __forceinline__ void bw_magic(MagicLane &ml, const typename VecT<VW>::type (*v)[IT], int nv, int j0) {
+  for (int jj = 0; jj < nv; ++jj) ml_add<IT, VW>(ml, v[jj], static_cast<uint32_t>(j0 + jj));
+}
+
+template <int R, int IT, int VW>
+__device__ __forceinline__ void bw_magic_out(MagicLane &ml, int K, const typename VecT<VW>::type (&acc)[IT][R]) {
+  typedef typename VecT<VW>::type V;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    V o[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) o[it] = acc[it][r];
+    ml_add<IT, VW>(ml, o, static_cast<uint32_t>(K + r));
   }
 }
 
@@ -291,7 +319,7 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
     for (int it = 0; it < IT; ++it)
 #pragma unroll
       for (int r = 0; r < R; ++r) acc[it][r] = 0u;
-    uint64_t mas = 0, mbs = 0;  // fused magic partial sums (MG only)
+    MagicLane ml;  // fused magic partial sums (MG only)
 
     if (full) {
       if constexpr (KC > 0) {
@@ -311,7 +339,7 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
 #pragma unroll
           for (int j = 0; j < KC; ++j) bw_accumulate<R, IT, VW>(acc, v[j], cells, K, j);
         }
-        if constexpr (MG) bw_magic<R, IT, VW>(a, s, off0, K, v, KC, 0, mas, mbs);
+        if constexpr (MG) bw_magic<R, IT, VW>(ml, v, KC, 0);
       } else {
         for (int j0 = 0; j0 < K; j0 += 4) {
           V v[4][IT];
@@ -333,7 +361,7 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
             for (int jj = 0; jj < 4; ++jj)
               if (jj < nj) bw_accumulate<R, IT, VW>(acc, v[jj], cells, K, j0 + jj);
           }
-          if constexpr (MG) bw_magic<R, IT, VW>(a, s, off0, K, v, nj, j0, mas, mbs);
+          if constexpr (MG) bw_magic<R, IT, VW>(ml, v, nj, j0);
         }
       }
 #pragma unroll
@@ -362,7 +390,7 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
         bw_acc1<R, IT, VW, BF, X0>(acc, v, cells, K, j);
         if constexpr (MG) {
           const V(*vv)[IT] = &v;
-          bw_magic<R, IT, VW>(a, s, off0, K, vv, 1, j, mas, mbs);
+          bw_magic<R, IT, VW>(ml, vv, 1, j);
         }
       }
 #pragma unroll
@@ -383,8 +411,8 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
       }
     }
     if constexpr (MG) {
-      bw_magic_out<R, IT, VW>(a, off0, K, acc, mas, mbs);
-      magic_commit(a.magic_acc, s, mas, mbs, red);
+      bw_magic_out<R, IT, VW>(ml, K, acc);
+      ml_commit(ml, a.magic_acc, s, K + R, static_cast<uint64_t>(a.size), static_cast<uint64_t>(off0), kStep, red);
     }
   }
 }
@@ -406,10 +434,12 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bytewise(ApplyArgs a) {
 
 // ------------------------------------------------------------------ bitsliced
 // A lane owns DW consecutive dwords of packet-column space in one super-packet and reads
-// the same columns of all 8 packets of every input shard.
-template <int R, int KC, int DW>
+// the same columns of all 8 packets of every input shard.  MG: also the stripe magic of the
+// inputs and outputs (encode + je_cksum_calc in one pass, as the bytewise kernel does).
+template <int R, int KC, int DW, bool MG = false>
 __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
   typedef typename VecT<DW>::type V;
+  __shared__ uint32_t red[MG ? kBlock / 64 : 1];
   const int K = KC ? KC : a.K;
   const uint32_t P = static_cast<uint32_t>(a.packet);
   const uint32_t col_bytes = static_cast<uint32_t>(a.size / 8);  // nsuper * P
@@ -421,9 +451,13 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
   for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
     const uint32_t s = t / tiles_per_stripe;
     const uint32_t colb = (t - s * tiles_per_stripe) * kTile + threadIdx.x * (4 * DW);
-    if (colb >= col_bytes) continue;  // only in a ragged last tile (P % 16 == 0 keeps a lane's DW dwords inside one packet)
+    // lanes past the end occur only in a ragged last tile (P % 16 == 0 keeps a lane's DW
+    // dwords inside one packet); with MG they still join the block's magic reduction
+    const bool valid = colb < col_bytes;
+    if (!MG && !valid) continue;
     const uint32_t sp = colb / P;
     const int64_t off = static_cast<int64_t>(sp) * 8 * P + (colb - sp * P);
+    MagicLane ml;
 
     V acc[R][8];
 #pragma unroll
@@ -431,11 +465,12 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
 #pragma unroll
       for (int x = 0; x < 8; ++x) acc[r][x] = 0u;
 
-    for (int j = 0; j < K; ++j) {
+    for (int j = 0; j < K && valid; ++j) {
       const uint64_t p = a.in[j].base + s * a.in[j].stride + off;
       V e[8];
 #pragma unroll
       for (int x = 0; x < 8; ++x) e[x] = __builtin_nontemporal_load(gptr<V>(p + x * P));
+      if constexpr (MG) ml_add<8, DW>(ml, e, static_cast<uint32_t>(j));
       uint32_t c[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) c[r] = cells[r * K + j].coef;
@@ -460,12 +495,16 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
         }
       }
     }
+    if (valid) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
+      for (int r = 0; r < R; ++r) {
+        const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
 #pragma unroll
-      for (int x = 0; x < 8; ++x) __builtin_nontemporal_store(acc[r][x], gptr_w<V>(q + x * P));
+        for (int x = 0; x < 8; ++x) __builtin_nontemporal_store(acc[r][x], gptr_w<V>(q + x * P));
+        if constexpr (MG) ml_add<8, DW>(ml, acc[r], static_cast<uint32_t>(K + r));
+      }
     }
+    if constexpr (MG) ml_commit(ml, a.magic_acc, s, K + R, static_cast<uint64_t>(a.size), static_cast<uint64_t>(off), P, red);
   }
 }
 
@@ -651,20 +690,29 @@ hipError_t dispatch_bytewise(const ApplyArgs &a, hipStream_t st, int grid, int s
   }
 }
 
+// encode + magic: 2 x 16 B per lane, 16 B for K >= 16 (as bytewise_shape; keep in step with
+// bytewise_magic_it in ec_kernels.hip)
 template <int R>
 hipError_t dispatch_bytewise_magic(const ApplyArgs &a, hipStream_t st, int grid) {
   switch (a.K) {
-#define LSEC_BWM_K(KK) \
-  case KK: hipLaunchKernelGGL((k_gf8_bytewise<R, KK, 2, true, 4, true>), dim3(grid), dim3(kBlock), 0, st, a); break;
-    LSEC_BWM_K(4) LSEC_BWM_K(6) LSEC_BWM_K(8) LSEC_BWM_K(10) LSEC_BWM_K(12) LSEC_BWM_K(16) LSEC_BWM_K(20)
+#define LSEC_BWM_K(KK, IT) \
+  case KK: hipLaunchKernelGGL((k_gf8_bytewise<R, KK, IT, true, 4, true>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    LSEC_BWM_K(4, 2) LSEC_BWM_K(6, 2) LSEC_BWM_K(8, 2) LSEC_BWM_K(10, 2) LSEC_BWM_K(12, 2) LSEC_BWM_K(16, 1) LSEC_BWM_K(20, 1)
 #undef LSEC_BWM_K
-    default: hipLaunchKernelGGL((k_gf8_bytewise<R, 0, 2, true, 4, true>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    default:
+      if (a.K >= 16) hipLaunchKernelGGL((k_gf8_bytewise<R, 0, 1, true, 4, true>), dim3(grid), dim3(kBlock), 0, st, a);
+      else hipLaunchKernelGGL((k_gf8_bytewise<R, 0, 2, true, 4, true>), dim3(grid), dim3(kBlock), 0, st, a);
+      break;
   }
   return hipGetLastError();
 }
 
 template <int R>
 hipError_t dispatch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid, int dw) {
+  if (a.magic_acc) {  // encode + stripe magic, one lane dword wide
+    hipLaunchKernelGGL((k_gf8_bitsliced<R, 0, 1, true>), dim3(grid), dim3(kBlock), 0, st, a);
+    return hipGetLastError();
+  }
   switch (dw) {
     case 4: hipLaunchKernelGGL((k_gf8_bitsliced<R, 0, 4>), dim3(grid), dim3(kBlock), 0, st, a); break;
     case 2: hipLaunchKernelGGL((k_gf8_bitsliced<R, 0, 2>), dim3(grid), dim3(kBlock), 0, st, a); break;
