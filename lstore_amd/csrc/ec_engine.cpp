@@ -63,6 +63,8 @@ int fail(const char *fmt, ...) {
 
 enum KernelKind { KNONE = 0, KBYTEWISE = 1, KBITSLICED = 2, KBITMATRIX = 3, KWORDWISE = 4 };
 
+constexpr int kMaxM = 64;  // parity devices per stripe (output shard tables below are sized for it)
+
 struct DecodeEntry {
   lsec::gf8::DecodePlan dp;
   std::map<int, CoefCell *> dev_cells;  // device -> e x k cells
@@ -444,7 +446,7 @@ int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, con
 int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
   const int k = p->data_strips, m = p->parity_strips;
   if (k < 1 || k > lsec::kMaxK) return fail("k=%d outside 1..%d", k, lsec::kMaxK);
-  if (m < 1) return fail("m=%d", m);
+  if (m < 1 || m > kMaxM) return fail("m=%d outside 1..%d", m, kMaxM);
   if (block_size < 0 || block_size % 8 != 0) return fail("block_size %lld is not a multiple of 8", block_size);
   const int kind = kernel_kind(p->method, p->w);
   if (kind == KNONE)
@@ -506,8 +508,7 @@ int encode_dev(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C, hi
   if (encode_cells(e, &cells)) return -1;
   const int k = p->data_strips;
   const int R = encode_rows(e);  // m (2 for r6, 1 for raid4)
-  ShardRef in[lsec::kMaxK], out[64];
-  if (R > 64) return fail("m=%d too large", R);
+  ShardRef in[lsec::kMaxK], out[kMaxM];
   for (int j = 0; j < k; ++j) in[j] = {reinterpret_cast<uint64_t>(sh[j].base), sh[j].stride};
   for (int r = 0; r < R; ++r) out[r] = {reinterpret_cast<uint64_t>(sh[k + r].base), sh[k + r].stride};
   return enqueue_apply(kernel_kind(p->method, p->w), cells, k, R, in, out, nstripes, C, p->packet_size, st, p->w);
@@ -528,7 +529,7 @@ int decode_dev(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C, co
   const void *cells = nullptr;
   if (decode_entry(e, ids, &ent, &cells)) return -1;
   const int k = p->data_strips;
-  ShardRef in[lsec::kMaxK], out[64];
+  ShardRef in[lsec::kMaxK], out[kMaxM];
   for (int j = 0; j < k; ++j) {
     const lsec_shard_t &s = sh[ent->dp.survivors[j]];
     in[j] = {reinterpret_cast<uint64_t>(s.base), s.stride};
@@ -884,7 +885,7 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
       if (err == hipSuccess) err = hipEventRecord(sl.in_done, stg->s_in);
       if (err == hipSuccess) err = hipStreamWaitEvent(stg->s_out, sl.in_done, 0);
       if (err != hipSuccess) { rc = fail("H2D: %s", hipGetErrorString(err)); break; }
-      ShardRef in[lsec::kMaxK], out[64];
+      ShardRef in[lsec::kMaxK], out[kMaxM];
       for (int j = 0; j < nin; ++j)
         in[j] = {reinterpret_cast<uint64_t>(sl.d) + static_cast<uint64_t>(j) * len, static_cast<int64_t>(nin * len)};
       for (int r = 0; r < nout; ++r)
@@ -1179,7 +1180,7 @@ class Dispatcher {
       const int nin = static_cast<int>(r0.in_ids.size()), nout = static_cast<int>(r0.out_ids.size());
       const size_t in_bytes = static_cast<size_t>(g.nstripes) * nin * C;
       char *dbase = sl.d + g.off;
-      ShardRef in[lsec::kMaxK], out[64];
+      ShardRef in[lsec::kMaxK], out[kMaxM];
       for (int j = 0; j < nin; ++j)
         in[j] = {reinterpret_cast<uint64_t>(dbase) + static_cast<uint64_t>(j) * C, static_cast<int64_t>(nin * C)};
       for (int o = 0; o < nout; ++o)

@@ -21,7 +21,7 @@
 
 namespace lsec {
 
-constexpr int kMaxK = 32;   // data devices per stripe the kernels accept
+constexpr int kMaxK = 64;   // data devices per stripe the kernels accept (LSEC_MAX_DEVS bounds k + m)
 constexpr int kMaxR = 16;   // output shards per launch
 
 struct ShardRef {

@@ -274,6 +274,42 @@ def test_xor_row_and_wide_shapes_vs_oracle(cuda, method, k, m, size):
             assert np.array_equal(sh, full), pat
 
 
+@pytest.mark.parametrize("method,k,m,size", [
+    (L.REED_SOL_VAN, 40, 4, 8192),        # k beyond the compile-time K list: generic-K kernel
+    (L.CAUCHY_GOOD, 40, 4, 8 * 64 * 4),
+    (L.REED_SOL_VAN, 48, 16, 4096),       # k + m = 64 (LSEC_MAX_DEVS), R = 16: two 8-row launches
+    (L.CAUCHY_ORIG, 30, 34, 8 * 32 * 2),  # k + m = 64 with more parity than data
+])
+def test_wide_stripes_vs_oracle(cuda, method, k, m, size):
+    """The widest stripes the engine takes (k + m <= 64): encode, stripe magic and erasures of
+    up to min(m, 6) devices, bit-exact vs the oracle and zlib."""
+    n = 2
+    P = 64 if method == L.CAUCHY_GOOD else (32 if method == L.CAUCHY_ORIG else 0)
+    st = np.zeros((n, k + m, size), dtype=np.uint8)
+    st[:, :k] = np.random.default_rng(k + m).integers(0, 256, (n, k, size), dtype=np.uint8)
+    with L.Plan.new(method, size, k, m, 8, P or 8, 8) as p:
+        assert p.form_encoding_matrix() == 0 and p.form_decoding_matrix() == 0
+        magic = p.encode_stripes_magic(st)
+        for s in range(n):
+            assert np.array_equal(st[s, k:], O.encode(method, st[s, :k], m, P)), s
+            assert np.array_equal(magic[s], _je_magic(st[s])), s
+        full = st.copy()
+        for pat in ([0], [k + m - 1], list(range(min(m, 6))), [1, k, k + 1][: m]):
+            st[:, pat] = 0x42
+            p.decode_stripes(st, pat)
+            assert np.array_equal(st, full), pat
+
+
+def test_stripe_width_limits_are_errors(cuda):
+    """m > 64 (LSEC_MAX_DEVS) is refused with a message, never written past a table."""
+    k, m, size = 4, 65, 4096
+    with L.Plan.new(L.REED_SOL_VAN, size, k, m, 8, 8, 8) as p:
+        assert p.form_encoding_matrix() == 0
+        st = np.zeros((1, k + m, size), np.uint8)
+        with pytest.raises(L.ErasureError, match="m=65"):
+            p.encode_stripes(st)
+
+
 @pytest.mark.parametrize("P", [8, 16, 24, 40, 4096])
 def test_bitsliced_packet_sizes(cuda, P):
     k, m = 6, 3
