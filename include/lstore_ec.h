@@ -194,6 +194,14 @@ int lsec_segment_inspect(lio_erasure_plan_t *plan, char *buf, int nstripes, int 
  * so the first lsec_decode_dev of that pattern does no host work.  0 / -1. */
 int lsec_prepare_decode(lio_erasure_plan_t *plan, const int *erasures);
 
+/* Devices that serve host-memory calls (et_*_stripes, et_*_magic, the plan's fn-pointers,
+ * lsec_segment_write).  n = 0 (the default): the calling thread's current HIP device.  With a
+ * set, a batch larger than the coalescing limit is split into contiguous stripe ranges, one
+ * per listed device, each staged and computed on its own device and PCIe link in parallel;
+ * smaller calls go to the listed devices in turn.  A device may be listed more than once.
+ * 0 / -1 (unknown device). */
+int lsec_set_host_devices(const int *devices, int n);
+
 /* Engine information / control */
 int lsec_abi_version(void);
 int lsec_device_count(void);                 /* visible HIP devices, 0 if none */

@@ -1273,6 +1273,63 @@ int run_host_auto(PlanExt *e, char **ptrs, int nstripes, long long C, const std:
   return run_host(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
 }
 
+// ---------------------------------------------------------------- host-path device set
+// Host-memory calls run on the caller's current device unless lsec_set_host_devices() named a
+// device set.  Then a batch above the coalescing limit is cut into contiguous stripe ranges,
+// one per device, each driven by its own thread through that device's staging pipeline and
+// PCIe link -- SURVEY §8e's static partition inside one LStore process -- and smaller calls go
+// to the devices' dispatchers in turn.  Matrix images are per device (encode_cells /
+// decode_entry are called on the device that runs the range).
+std::mutex g_devs_mu;
+std::vector<int> g_host_devs;  // empty: the caller's current device
+
+std::vector<int> host_devices() {
+  std::lock_guard<std::mutex> lk(g_devs_mu);
+  return g_host_devs;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (dev != prev) ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+template <typename F>
+int on_host_devices(int nstripes, size_t bytes, F &&fn) {
+  const std::vector<int> devs = host_devices();
+  if (devs.empty()) return fn(0, nstripes);
+  if (devs.size() == 1 || nstripes < 2 || bytes <= coalesce_limit()) {
+    static std::atomic<unsigned> rr{0};
+    const int dev = devs[rr.fetch_add(1) % devs.size()];
+    DeviceGuard g(dev);
+    if (!g.ok) return fail("cannot select device %d", dev);
+    return fn(0, nstripes);
+  }
+  const int G = std::min(static_cast<int>(devs.size()), nstripes);
+  std::vector<int> rc(G, 0);
+  std::vector<std::string> err(G);
+  auto work = [&](int g) {
+    const int base = nstripes / G, extra = nstripes % G;
+    const int s0 = g * base + std::min(g, extra), n = base + (g < extra ? 1 : 0);
+    DeviceGuard dg(devs[g]);
+    rc[g] = dg.ok ? fn(s0, n) : fail("cannot select device %d", devs[g]);
+    if (rc[g]) err[g] = tl_err;  // tl_err is per thread
+  };
+  std::vector<std::thread> th;
+  for (int g = 1; g < G; ++g) th.emplace_back(work, g);
+  work(0);
+  for (auto &t : th) t.join();
+  for (int g = 0; g < G; ++g)
+    if (rc[g]) return fail("device %d: %s", devs[g], err[g].c_str());
+  return 0;
+}
+
 int encode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C) {
   lio_erasure_plan_t *p = &e->pub;
   if (!ptrs) return fail("ptrs is NULL");
@@ -1286,14 +1343,17 @@ int encode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C) {
     HIP_OK(hipStreamSynchronize(st));
     return 0;
   }
-  const void *cells = nullptr;
-  if (encode_cells(e, &cells)) return -1;
-  const int k = p->data_strips;
+  if (ensure_coding(e)) return -1;
+  const int k = p->data_strips, km = k + p->parity_strips;
   const int R = encode_rows(e);
   std::vector<int> in_ids(k), out_ids(R);
   for (int j = 0; j < k; ++j) in_ids[j] = j;
   for (int r = 0; r < R; ++r) out_ids[r] = k + r;
-  return run_host_auto(e, ptrs, nstripes, C, in_ids, out_ids, cells, kernel_kind(p->method, p->w));
+  return on_host_devices(nstripes, static_cast<size_t>(nstripes) * (k + R) * C, [&](int s0, int n) {
+    const void *cells = nullptr;
+    if (encode_cells(e, &cells)) return -1;
+    return run_host_auto(e, ptrs + static_cast<size_t>(s0) * km, n, C, in_ids, out_ids, cells, kernel_kind(p->method, p->w));
+  });
 }
 
 int decode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C, const int *erasures) {
@@ -1314,10 +1374,14 @@ int decode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C, cons
     HIP_OK(hipStreamSynchronize(st));
     return 0;
   }
-  DecodeEntry *ent = nullptr;
-  const void *cells = nullptr;
-  if (decode_entry(e, ids, &ent, &cells)) return -1;
-  return run_host_auto(e, ptrs, nstripes, C, ent->dp.survivors, ent->dp.erased, cells, kernel_kind(p->method, p->w));
+  const int km = p->data_strips + p->parity_strips;
+  return on_host_devices(nstripes, static_cast<size_t>(nstripes) * (p->data_strips + ids.size()) * C, [&](int s0, int n) {
+    DecodeEntry *ent = nullptr;
+    const void *cells = nullptr;
+    if (decode_entry(e, ids, &ent, &cells)) return -1;
+    return run_host_auto(e, ptrs + static_cast<size_t>(s0) * km, n, C, ent->dp.survivors, ent->dp.erased, cells,
+                         kernel_kind(p->method, p->w));
+  });
 }
 
 int encode_stripes_magic_impl(PlanExt *e, char **ptrs, int nstripes, long long C, uint8_t *magic) {
@@ -1325,15 +1389,19 @@ int encode_stripes_magic_impl(PlanExt *e, char **ptrs, int nstripes, long long C
   if (!ptrs || !magic) return fail("ptrs / magic is NULL");
   if (check_geometry(p, C)) return -1;
   if (nstripes <= 0 || C == 0) return 0;
-  const void *cells = nullptr;
-  if (encode_cells(e, &cells)) return -1;
-  const int k = p->data_strips;
+  if (ensure_coding(e)) return -1;
+  const int k = p->data_strips, km = k + p->parity_strips;
   const int R = encode_rows(e);
   if (R != p->parity_strips) return fail("stripe magic needs m parity rows");
   std::vector<int> in_ids(k), out_ids(R);
   for (int j = 0; j < k; ++j) in_ids[j] = j;
   for (int r = 0; r < R; ++r) out_ids[r] = k + r;
-  return run_host(e, ptrs, nstripes, C, in_ids, out_ids, cells, kernel_kind(p->method, p->w), magic);
+  return on_host_devices(nstripes, static_cast<size_t>(nstripes) * km * C, [&](int s0, int n) {
+    const void *cells = nullptr;
+    if (encode_cells(e, &cells)) return -1;
+    return run_host(e, ptrs + static_cast<size_t>(s0) * km, n, C, in_ids, out_ids, cells, kernel_kind(p->method, p->w),
+                    magic + 4 * static_cast<size_t>(s0));
+  });
 }
 
 int stripes_magic_impl(PlanExt *e, char **ptrs, int nstripes, long long C, uint8_t *magic) {
@@ -1344,7 +1412,10 @@ int stripes_magic_impl(PlanExt *e, char **ptrs, int nstripes, long long C, uint8
   const int km = p->data_strips + p->parity_strips;
   std::vector<int> in_ids(km), none;
   for (int i = 0; i < km; ++i) in_ids[i] = i;
-  return run_host(e, ptrs, nstripes, C, in_ids, none, nullptr, KBYTEWISE, magic);
+  return on_host_devices(nstripes, static_cast<size_t>(nstripes) * km * C, [&](int s0, int n) {
+    return run_host(e, ptrs + static_cast<size_t>(s0) * km, n, C, in_ids, none, nullptr, KBYTEWISE,
+                    magic + 4 * static_cast<size_t>(s0));
+  });
 }
 
 int magic_dev_impl(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C, uint8_t *magic, hipStream_t st) {
@@ -2002,6 +2073,25 @@ int lsec_prepare_decode(lio_erasure_plan_t *plan, const int *erasures) {
   DecodeEntry *ent = nullptr;
   const void *cells = nullptr;
   return decode_entry(e, ids, &ent, &cells);
+}
+
+int lsec_set_host_devices(const int *devices, int n) {
+  std::vector<int> v;
+  if (n > 0) {
+    if (!devices) return fail("devices is NULL");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail("no HIP device");
+    }
+    for (int i = 0; i < n; ++i) {
+      if (devices[i] < 0 || devices[i] >= count) return fail("device %d outside 0..%d", devices[i], count - 1);
+      v.push_back(devices[i]);
+    }
+  }
+  std::lock_guard<std::mutex> lk(g_devs_mu);
+  g_host_devs.swap(v);
+  return 0;
 }
 
 int lsec_abi_version(void) { return LSEC_ABI_VERSION; }

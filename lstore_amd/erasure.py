@@ -73,7 +73,7 @@ EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan",
            "lsec_decode_dev", "et_encode_stripes_magic", "et_stripes_magic", "lsec_encode_magic_dev",
            "lsec_stripe_magic_dev", "lsec_segment_write", "lsec_segment_read", "lsec_segment_inspect",
            "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count", "lsec_last_error", "lsec_plan_kernel",
-           "lsec_set_kernel_variant")
+           "lsec_set_kernel_variant", "lsec_set_host_devices")
 
 # read / inspect flags and stripe states (include/lstore_ec.h)
 READ_PARANOID, MAGIC_LEGACY, INSPECT_FIX, MAX_DEVS = 1, 2, 4, 64
@@ -140,6 +140,7 @@ def lib():
     L.lsec_plan_kernel.argtypes = [P]
     L.lsec_set_kernel_variant.argtypes = [C.c_int, C.c_int]
     L.lsec_set_kernel_variant.restype = None
+    L.lsec_set_host_devices.argtypes = [C.POINTER(C.c_int), C.c_int]
     _lib = L
     return L
 
@@ -429,6 +430,12 @@ def _stream_handle(stream) -> int:
 
 def device_count() -> int:
     return lib().lsec_device_count()
+
+
+def set_host_devices(devices: Sequence[int] = ()) -> None:
+    """lsec_set_host_devices: devices serving host-memory calls (empty = the current device)."""
+    arr = (C.c_int * max(1, len(devices)))(*devices)
+    _check(lib().lsec_set_host_devices(arr, len(devices)), "lsec_set_host_devices")
 
 
 def set_kernel_variant(bytewise: int = 0, bitsliced: int = 0) -> None:

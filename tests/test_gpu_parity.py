@@ -483,6 +483,38 @@ def test_fn_pointer_pinned_and_pageable_callers_coalesced(cuda):
         assert not errors, errors
 
 
+@pytest.mark.parametrize("devices", [(0, 0), (0, 0, 0)])
+def test_host_batches_split_over_device_set(cuda, devices):
+    """lsec_set_host_devices: a large host batch is cut into stripe ranges driven by one thread
+    per listed device (here the one GPU listed several times), small calls round-robin; results
+    identical to the oracle, including magics and decodes."""
+    from lstore_amd import erasure as E
+
+    k, m, size, n = 6, 3, 1 << 20, 23
+    st = np.zeros((n, k + m, size), dtype=np.uint8)
+    st[:, :k] = np.random.default_rng(len(devices)).integers(0, 256, (n, k, size), dtype=np.uint8)
+    E.set_host_devices(devices)
+    try:
+        with L.Plan.for_chunk(L.CAUCHY_GOOD, k, m, size) as p:
+            magic = p.encode_stripes_magic(st)
+            for s in range(n):
+                assert np.array_equal(st[s, k:], O.encode(O.CAUCHY_GOOD, st[s, :k], m, p.packet_size)), s
+                assert np.array_equal(magic[s], _je_magic(st[s])), s
+            assert np.array_equal(p.stripes_magic(st), magic)
+            keep = st[:, [2, k]].copy()
+            st[:, [2, k]] = 0
+            p.decode_stripes(st, [2, k])
+            assert np.array_equal(st[:, [2, k]], keep)
+            one = st[5].copy()                       # a single small call (round-robin path)
+            one[k:] = 0
+            p.encode_block([one[i] for i in range(k + m)])
+            assert np.array_equal(one, st[5])
+    finally:
+        E.set_host_devices(())
+    with pytest.raises(L.ErasureError, match="outside"):
+        E.set_host_devices((0, 99))
+
+
 # ---------------------------------------------------------------- stripe magic (adler32, segment/jerasure.c:169-182)
 def _je_magic(full):
     """je_cksum_calc: adler32 over the k+m chunks in order, 4 bytes little-endian (zlib)."""

@@ -172,6 +172,14 @@ def test_no_gpu_means_loud_failure(built):
         assert rc == -1 and E.last_error()
 
 
+def test_host_device_set_without_gpu(built):
+    """lsec_set_host_devices: clearing the set always works; naming a device needs one."""
+    E.set_host_devices(())
+    if E.device_count() == 0:
+        with pytest.raises(E.ErasureError):
+            E.set_host_devices((0,))
+
+
 def test_unsupported_method_is_an_error_not_a_fallback(built):
     with L.Plan.new(L.LIBERATION, 0, 6, 2, 37, 8, 8) as p:   # a prime w outside the instantiated list
         assert p.kernel == 0
