@@ -40,6 +40,20 @@ def run_pass(counter, outdir, bench_args):
     return per_kernel
 
 
+def annotate(res, extra):
+    """Geometry of the bench run and, per kernel, algorithmic bytes and traffic per stripe
+    (bench.py reads traffic_per_stripe back for its roofline.traffic field)."""
+    def arg(name, default):
+        return int(extra[extra.index(name) + 1]) if name in extra else default
+    k, m, C, N = arg("--k", 6), arg("--m", 3), arg("--chunk", 1 << 20), arg("--stripes", 4096)
+    res.update({"bench_stripes": N, "chunk": C, "k": k, "m": m})
+    for name, v in res["kernels"].items():
+        R = int(name.split("<")[1].split(",")[0])  # output rows: m (encode) or erased shards (decode)
+        v["algorithmic"] = (k + R) * C * N
+        v["traffic_over_algorithmic"] = round(v["traffic"] / v["algorithmic"], 4)
+        v["traffic_per_stripe"] = v["traffic"] / N
+
+
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     extra = sys.argv[2:]
@@ -57,6 +71,7 @@ def main():
         w = sorted(write.get(name, [0]))[len(write.get(name, [0])) // 2] * 1024
         res["kernels"][name] = {"fetch_raw": f, "fetch_corrected": 2 * f, "write": w,
                                 "traffic": 2 * f + w, "dispatches": len(fetch.get(name, []))}
+    annotate(res, extra)
     path = os.path.join(ROOT, "gpurun_out", f"{tag}_pmc_traffic.json")
     with open(path, "w") as fh:
         json.dump(res, fh, indent=1)

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Kernel-trace summary from a rocprofv3 rocpd database (the default output on ROCm 7.2).
+"""Kernel-trace summary per (kernel, grid) from rocprofv3 output: the rocpd database (the
+default output on ROCm 7.2) or the --output-format csv kernel trace.
 
 python tools/rocpd_stats.py gpurun_out/prof_x/run_results.db [out.csv] [--all]
+python tools/rocpd_stats.py gpurun_out/prof_x/run_kernel_trace.csv [out.csv] [--all]
 
 Writes Name,GridX,Calls,AverageNs,MinNs,MaxNs,VGPRs,SGPRs per (kernel, grid) -- the same
 columns as the profiles/*_kernel_stats.csv summaries -- for the engine's kernels (lsec::)
@@ -15,11 +17,23 @@ import sys
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     every = "--all" in sys.argv
-    db = sqlite3.connect(args[0])
-    rows = db.execute(
-        "select name, grid_x, count(*), avg(duration), min(duration), max(duration), "
-        "max(vgpr_count + accum_vgpr_count), max(sgpr_count) from kernels group by name, grid_x "
-        "order by sum(duration) desc").fetchall()
+    if args[0].endswith(".csv"):
+        groups = {}
+        for r in csv.DictReader(open(args[0])):
+            key = (r["Kernel_Name"], int(r["Grid_Size_X"]))
+            d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            g = groups.setdefault(key, [[], 0, 0])
+            g[0].append(d)
+            g[1] = max(g[1], int(r["VGPR_Count"]) + int(r["Accum_VGPR_Count"]))
+            g[2] = max(g[2], int(r["SGPR_Count"]))
+        rows = [(n, gx, len(v), sum(v) / len(v), min(v), max(v), vg, sg) for (n, gx), (v, vg, sg) in groups.items()]
+        rows.sort(key=lambda r: -r[2] * r[3])
+    else:
+        db = sqlite3.connect(args[0])
+        rows = db.execute(
+            "select name, grid_x, count(*), avg(duration), min(duration), max(duration), "
+            "max(vgpr_count + accum_vgpr_count), max(sgpr_count) from kernels group by name, grid_x "
+            "order by sum(duration) desc").fetchall()
     out = open(args[1], "w", newline="") if len(args) > 1 else sys.stdout
     w = csv.writer(out, quoting=csv.QUOTE_MINIMAL)
     w.writerow(["Name", "GridX", "Calls", "AverageNs", "MinNs", "MaxNs", "VGPRs", "SGPRs"])
