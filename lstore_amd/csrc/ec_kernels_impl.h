@@ -472,8 +472,12 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
       for (int x = 0; x < 8; ++x) e[x] = __builtin_nontemporal_load(gptr<V>(p + x * P));
       if constexpr (MG) ml_add<8, DW>(ml, e, static_cast<uint32_t>(j));
       uint32_t c[R];
+      uint32_t cm = 0;  // bits used by any output: no doublings past the highest one
 #pragma unroll
-      for (int r = 0; r < R; ++r) c[r] = cells[r * K + j].coef;
+      for (int r = 0; r < R; ++r) {
+        c[r] = cells[r * K + j].coef;
+        cm |= c[r];
+      }
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
 #pragma unroll
@@ -482,6 +486,7 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
 #pragma unroll
             for (int x = 0; x < 8; ++x) acc[r][x] ^= e[x];
           }
+        if ((cm >> (b + 1)) == 0) break;  // e.g. the XOR rows of a single-erasure decode
         if (b < 7) {  // e <- 2*e in bit-sliced form
           const V top = e[7];
           e[7] = e[6];
