@@ -10,6 +10,11 @@ path; the only collectives are the timing barrier and the max-over-ranks reducti
 
 value = k*C*N*world / max_rank(step time) / 2^30  (data GiB/s, "N KiB stripes" = C per shard)
 
+Device-resident layout: data [N][k][C], parity [N][m][C], every shard row followed by --pad
+(default 1024) unused bytes, so the k+m streams of a stripe do not start on the same HBM
+channel (shards exactly 1 MiB apart cost the encode ~8 %: profiles/r01_v15_pad_ab.txt).
+layout.unpadded reports the same stripes with shards exactly C apart, launch-timed.
+
 Also reported (same JSON line):
   roofline      encode kernel: algorithmic HBM bytes (k+m)*C*N per launch / avg launch time
                 (HIP events on the launch stream) vs 8 TB/s
@@ -49,6 +54,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--variant", type=str, default="0,0", help="bytewise,bitsliced kernel variants")
+    ap.add_argument("--pad", type=int, default=1024,
+                    help="bytes left unused after every shard row in HBM (0 = shards exactly C apart)")
+    ap.add_argument("--no-layout-ab", action="store_true", help="skip the unpadded-layout comparison")
     return ap.parse_args()
 
 
@@ -180,32 +188,52 @@ def main():
     plan = L.Plan.for_chunk(method, k, m, C)
     P = plan.packet_size
 
-    # synthetic stripes, resident in HBM before timing (different per rank)
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    data = torch.randint(0, 256, (N, k, C), dtype=torch.uint8, device=dev, generator=g)
-    par = torch.empty((N, m, C), dtype=torch.uint8, device=dev)
-    rebuilt = torch.empty((N, 1, C), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
-
-    enc_refs, _, _ = plan.tensor_refs(data, par)
-    enc_arr = plan.shard_refs(enc_refs)
-    dec_refs = list(enc_refs)
-    dec_refs[a.lost] = (rebuilt.data_ptr(), rebuilt.stride(0))
-    dec_arr = plan.shard_refs(dec_refs)
     er = E._erasure_array([a.lost])
     plan.prepare_decode([a.lost])
     lib = E.lib()
 
-    def encode():
-        rc = lib.lsec_encode_dev(plan.ptr, enc_arr, N, C, sh)
-        if rc:
-            raise E.ErasureError(E.last_error())
+    def workload(pad, seed):
+        """Synthetic stripes resident in HBM: data [N][k][C], parity [N][m][C] and the rebuilt
+        shard [N][1][C], every shard row followed by `pad` unused bytes (the device-resident
+        layout).  Returns the tensors and the encode / decode launchers."""
+        g = torch.Generator(device=dev).manual_seed(seed)
+        data = torch.randint(0, 256, (N, k, C + pad), dtype=torch.uint8, device=dev, generator=g)[:, :, :C]
+        par = torch.empty((N, m, C + pad), dtype=torch.uint8, device=dev)[:, :, :C]
+        rebuilt = torch.empty((N, 1, C + pad), dtype=torch.uint8, device=dev)[:, :, :C]
+        enc_refs, _, _ = plan.tensor_refs(data, par)
+        enc_arr = plan.shard_refs(enc_refs)
+        dec_refs = list(enc_refs)
+        dec_refs[a.lost] = (rebuilt.data_ptr(), rebuilt.stride(0))
+        dec_arr = plan.shard_refs(dec_refs)
 
-    def decode():
-        rc = lib.lsec_decode_dev(plan.ptr, dec_arr, N, C, er, sh)
-        if rc:
-            raise E.ErasureError(E.last_error())
+        def encode():
+            rc = lib.lsec_encode_dev(plan.ptr, enc_arr, N, C, sh)
+            if rc:
+                raise E.ErasureError(E.last_error())
+
+        def decode():
+            rc = lib.lsec_decode_dev(plan.ptr, dec_arr, N, C, er, sh)
+            if rc:
+                raise E.ErasureError(E.last_error())
+
+        return data, par, rebuilt, encode, decode
+
+    def launch_times(encode, decode, reps):
+        """average encode / decode launch time (s), HIP events on the launch stream"""
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record(stream)
+        for _ in range(reps):
+            encode()
+        ev[1].record(stream)
+        for _ in range(reps):
+            decode()
+        ev[2].record(stream)
+        torch.cuda.synchronize()
+        return ev[0].elapsed_time(ev[1]) / 1e3 / reps, ev[1].elapsed_time(ev[2]) / 1e3 / reps
+
+    data, par, rebuilt, encode, decode = workload(a.pad, 1234 + rank)
 
     for _ in range(a.warmup):
         encode()
@@ -230,17 +258,7 @@ def main():
 
     # ---- per-kernel timing with HIP events on the launch stream (roofline)
     reps = max(3, min(10, a.steps))
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    ev[0].record(stream)
-    for _ in range(reps):
-        encode()
-    ev[1].record(stream)
-    for _ in range(reps):
-        decode()
-    ev[2].record(stream)
-    torch.cuda.synchronize()
-    t_enc = ev[0].elapsed_time(ev[1]) / 1e3 / reps
-    t_dec = ev[1].elapsed_time(ev[2]) / 1e3 / reps
+    t_enc, t_dec = launch_times(encode, decode, reps)
 
     # ---- parity check (bit-exact vs the CPU oracle on sampled stripes)
     import oracle as O
@@ -259,12 +277,28 @@ def main():
         sys.exit(1)
 
     data_bytes = k * C * N
+    enc_hbm = (k + m) * C * N
+    dec_hbm = (k + 1) * C * N
+    layout = {"shard_pad_bytes": a.pad}
+    if a.pad and world == 1 and not a.no_layout_ab:
+        # the same stripes in the unpadded layout (shards exactly C apart, as one cache page
+        # holds them), launch-timed beside the padded one for the record
+        del data, par, rebuilt
+        torch.cuda.empty_cache()
+        _, _, _, enc0, dec0 = workload(0, 1234 + rank)
+        enc0()
+        dec0()
+        te0, td0 = launch_times(enc0, dec0, reps)
+        layout["unpadded"] = {"encode_frac": round(enc_hbm / te0 / HBM_PEAK, 4),
+                              "decode_frac": round(dec_hbm / td0 / HBM_PEAK, 4),
+                              "value_from_launch_times": round(data_bytes / (te0 + td0) / 2**30, 2),
+                              "padded_value_from_launch_times": round(data_bytes / (t_enc + t_dec) / 2**30, 2)}
+        del enc0, dec0
+        torch.cuda.empty_cache()
     if a.total_stripes > 0:
         value = k * C * a.total_stripes * a.steps / elapsed / 2**30
     else:
         value = data_bytes * world * a.steps / elapsed / 2**30
-    enc_hbm = (k + m) * C * N
-    dec_hbm = (k + 1) * C * N
     achieved = enc_hbm / t_enc
     traffic, traffic_src = pmc_traffic(k, m, C, N, plan.kernel)
 
@@ -305,6 +339,7 @@ def main():
                          "algorithmic_bytes_per_launch": enc_hbm, "avg_launch_ms": round(t_enc * 1e3, 4),
                          "decode_achieved_GBps": round(dec_hbm / t_dec / 1e9, 1),
                          "decode_frac": round(dec_hbm / t_dec / HBM_PEAK, 4)},
+            "layout": layout,
             "cpu_baseline": cpu,
             "host_path": host,
             "parity_check": "bit-exact vs oracle on stripes %s" % pick,

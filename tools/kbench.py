@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--configs", default="rs63,cg104,cg63")
     ap.add_argument("--variants", default="0,0;1,0;0,2;0,4")
     ap.add_argument("--magic", action="store_true", help="also time fused encode+magic and standalone magic")
+    ap.add_argument("--pad", type=int, default=0, help="bytes of padding after every shard (HBM channel spread)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     variants = [tuple(int(x) for x in v.split(",")) for v in a.variants.split(";")]
@@ -50,8 +51,8 @@ def main():
         w = CONFIGS[name][4] if len(CONFIGS[name]) > 4 else -1
         N = max(8, int(a.data_gib * 2**30 / (k * C)))
         plan = L.Plan.for_chunk(meth, k, m, C, w)
-        data = torch.randint(0, 256, (N, k, C), dtype=torch.uint8, device=dev)
-        par = torch.empty((N, m, C), dtype=torch.uint8, device=dev)
+        data = torch.randint(0, 256, (N, k, C + a.pad), dtype=torch.uint8, device=dev)[:, :, :C]
+        par = torch.empty((N, m, C + a.pad), dtype=torch.uint8, device=dev)[:, :, :C]
         out = torch.empty((N, 1, C), dtype=torch.uint8, device=dev)
         plan.encode_dev(data, par)
         ref_par = par.clone()
