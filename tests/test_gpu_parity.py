@@ -310,6 +310,49 @@ def test_stripe_width_limits_are_errors(cuda):
             p.encode_stripes(st)
 
 
+def test_randomized_plans_vs_oracle(cuda):
+    """Seeded random plans across methods, word sizes, k, m, chunk and packet sizes, with
+    random erasure sets: every parity and every rebuilt shard bit-exact vs the oracle."""
+    import torch
+
+    rng = np.random.default_rng(20261016)
+    checked = 0
+    for case in range(48):
+        method = int(rng.choice([L.REED_SOL_VAN, L.REED_SOL_R6_OP, L.CAUCHY_ORIG, L.CAUCHY_GOOD, L.RAID4]))
+        w = 8 if method == L.RAID4 or case % 4 else int(rng.choice([16, 32]))
+        k = int(rng.integers(1, 25))
+        m = 2 if method == L.REED_SOL_R6_OP else 1 if method == L.RAID4 else int(rng.integers(1, 9))
+        if method in (L.CAUCHY_ORIG, L.CAUCHY_GOOD):
+            P = 8 * int(rng.integers(1, 17))
+            size = w * P * int(rng.integers(1, 5))
+        else:
+            P = 0
+            size = 8 * int(rng.integers(1, 1025))
+        n = int(rng.integers(1, 4))
+        data = rng.integers(0, 256, (n, k, size), dtype=np.uint8)
+        with L.Plan.new(method, size, k, m, w, P or 8, 1 if method == L.RAID4 else 8) as p:
+            p.form_encoding_matrix()
+            p.form_decoding_matrix()
+            d = torch.from_numpy(data).to(cuda)
+            par = torch.zeros((n, m, size), dtype=torch.uint8, device=cuda)
+            p.encode_dev(d, par)
+            torch.cuda.synchronize()
+            hp = par.cpu().numpy()
+            for s in range(n):
+                assert np.array_equal(hp[s], O.encode(method, data[s], m, P, w)), (case, method, w, k, m, size, P)
+            full = np.concatenate([data, hp], axis=1)
+            e = int(rng.integers(1, m + 1))
+            lost = sorted(rng.choice(k + m, size=e, replace=False).tolist())
+            if method == L.RAID4 and lost[0] >= k:
+                continue  # raid4.c:48 leaves a lost parity alone
+            sh = full.copy()
+            sh[:, lost] = 0x99
+            p.decode_stripes(sh, lost)
+            assert np.array_equal(sh, full), (case, method, w, k, m, size, P, lost)
+            checked += 1
+    assert checked >= 40
+
+
 @pytest.mark.parametrize("P", [8, 16, 24, 40, 4096])
 def test_bitsliced_packet_sizes(cuda, P):
     k, m = 6, 3
