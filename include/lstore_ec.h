@@ -207,8 +207,9 @@ int lsec_abi_version(void);
 int lsec_device_count(void);                 /* visible HIP devices, 0 if none */
 const char *lsec_last_error(void);           /* thread-local message of the last failure */
 /* kernel that applies the plan: 1 = bytewise GF(2^8) (RS, r6, raid4), 2 = bit-sliced GF(2^8)
- * (Cauchy w = 8), 3 = GF(2) bitmatrix (liberation family; Cauchy w = 16/32), 4 = wordwise
- * GF(2^16) / GF(2^32) (RS, r6 at w = 16/32), 0 = no GPU kernel (calls fail with -1) */
+ * (Cauchy w = 8), 3 = GF(2) bitmatrix (liberation family), 4 = wordwise GF(2^16) / GF(2^32)
+ * (RS, r6 at w = 16/32), 5 = bit-sliced GF(2^16) / GF(2^32) (Cauchy at w = 16/32),
+ * 0 = no GPU kernel (calls fail with -1) */
 int lsec_plan_kernel(lio_erasure_plan_t *plan);
 void lsec_set_kernel_variant(int bytewise_variant, int bitsliced_variant);  /* tuning experiments */
 

@@ -61,7 +61,7 @@ int fail(const char *fmt, ...) {
     if (e_ != hipSuccess) return fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
   } while (0)
 
-enum KernelKind { KNONE = 0, KBYTEWISE = 1, KBITSLICED = 2, KBITMATRIX = 3, KWORDWISE = 4 };
+enum KernelKind { KNONE = 0, KBYTEWISE = 1, KBITSLICED = 2, KBITMATRIX = 3, KWORDWISE = 4, KBITSLICEDW = 5 };
 
 constexpr int kMaxM = 64;  // parity devices per stripe (output shard tables below are sized for it)
 
@@ -103,7 +103,7 @@ bool liberation_family(int method) { return method == BLAUM_ROTH || method == LI
 
 // Which kernel applies a plan:
 //   RS / r6 at w = 8 -> bytewise GF(2^8); at w = 16 / 32 -> wordwise GF(2^w)
-//   Cauchy at w = 8 -> bit-sliced GF(2^8); at w = 16 / 32 -> generic GF(2) bitmatrix
+//   Cauchy at w = 8 -> bit-sliced GF(2^8); at w = 16 / 32 -> bit-sliced GF(2^w)
 //   liberation family -> generic GF(2) bitmatrix; raid4 -> bytewise XOR (w unused, raid4.c)
 int kernel_kind(int method, int w) {
   if (liberation_family(method)) return lsec::bitmatrix_w_supported(w) ? KBITMATRIX : KNONE;
@@ -116,13 +116,14 @@ int kernel_kind(int method, int w) {
       return wide ? KWORDWISE : KBYTEWISE;
     case CAUCHY_ORIG:
     case CAUCHY_GOOD:
-      return wide ? KBITMATRIX : KBITSLICED;
+      return wide ? KBITSLICEDW : KBITSLICED;
     default:
       return KNONE;
   }
 }
 
-bool uses_u32_image(int kind) { return kind == KBITMATRIX || kind == KWORDWISE; }
+bool uses_u32_image(int kind) { return kind == KBITMATRIX || kind == KWORDWISE || kind == KBITSLICEDW; }
+bool packet_kind(int kind) { return kind == KBITSLICED || kind == KBITMATRIX || kind == KBITSLICEDW; }
 
 int *to_int_array(const lsec::gfw::Mat &m) {
   int *a = static_cast<int *>(malloc(sizeof(int) * m.size()));
@@ -253,7 +254,7 @@ int form_matrices(lio_erasure_plan_t *p, bool with_schedule) {
     e->impl->coding_ready = true;
   } else if (p->encode_matrix) {
     const int rows = (p->method == REED_SOL_R6_OP) ? 2 : m;
-    if (kind == KWORDWISE) {
+    if (kind == KWORDWISE || kind == KBITSLICEDW) {
       e->impl->coding_w.resize(static_cast<size_t>(rows) * k);
       for (size_t i = 0; i < e->impl->coding_w.size(); ++i) e->impl->coding_w[i] = static_cast<uint32_t>(p->encode_matrix[i]);
       e->impl->enc_masks = word_image(e->impl->coding_w, rows, k, w);
@@ -318,7 +319,7 @@ int upload_cells(const std::vector<CoefCell> &h, CoefCell **out) {
 int encode_rows(const PlanExt *e) {
   const int kind = kernel_kind(e->pub.method, e->pub.w);
   if (kind == KBITMATRIX) return e->pub.parity_strips;
-  if (kind == KWORDWISE) return static_cast<int>(e->impl->coding_w.size()) / e->pub.data_strips;
+  if (kind == KWORDWISE || kind == KBITSLICEDW) return static_cast<int>(e->impl->coding_w.size()) / e->pub.data_strips;
   return static_cast<int>(e->impl->coding.size()) / e->pub.data_strips;
 }
 
@@ -399,7 +400,7 @@ int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, con
   if (it == e->impl->decode_cache.end()) {
     DecodeEntry ent;
     const int k = e->pub.data_strips;
-    if (kind == KWORDWISE) {
+    if (kind == KWORDWISE || kind == KBITSLICEDW) {
       const int w = e->pub.w;
       const int m = static_cast<int>(e->impl->coding_w.size()) / k;
       lsec::gfw::DecodePlan wp;
@@ -451,7 +452,7 @@ int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
   const int kind = kernel_kind(p->method, p->w);
   if (kind == KNONE)
     return fail("method %s (w=%d) has no GPU kernel in this build", JE_method[p->method], p->w);
-  if (kind == KBITSLICED || kind == KBITMATRIX) {
+  if (packet_kind(kind)) {
     const long long sp = static_cast<long long>(p->w) * p->packet_size;
     if (p->packet_size <= 0 || p->packet_size % 4 != 0 || block_size % sp != 0)
       return fail("block_size %lld is not a multiple of w*packet_size = %lld", block_size, sp);
@@ -465,7 +466,7 @@ int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
 // KBITMATRIX the uint32 row masks [(r*w+l)*K + j].
 int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in, const ShardRef *out,
                   int nstripes, long long size, int packet, hipStream_t st, int w = 8) {
-  const int rmax = kind == KBITMATRIX ? 2 : 8;
+  const int rmax = kind == KBITMATRIX ? 2 : (kind == KBITSLICEDW && w == 32) ? 4 : 8;
   for (int r0 = 0; r0 < R; r0 += rmax) {
     lsec::ApplyArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -492,6 +493,7 @@ int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in,
       const hipError_t err = kind == KBYTEWISE    ? lsec::launch_bytewise(b, st)
                              : kind == KBITMATRIX ? lsec::launch_bitmatrix(b, st)
                              : kind == KWORDWISE  ? lsec::launch_wordwise(b, st)
+                             : kind == KBITSLICEDW ? lsec::launch_gfw_bitsliced(b, st)
                                                   : lsec::launch_bitsliced(b, st);
       if (err != hipSuccess) return fail("kernel launch failed: %s", hipGetErrorString(err));
     }
@@ -811,7 +813,7 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   long long cb = C;
   if (per_col * C > budget / 2) {
     // packet codes must cut at super-packet boundaries (w * P bytes)
-    const long long align = (kind == KBITSLICED || kind == KBITMATRIX) ? static_cast<long long>(p->w) * p->packet_size : 8192;
+    const long long align = packet_kind(kind) ? static_cast<long long>(p->w) * p->packet_size : 8192;
     cb = static_cast<long long>(budget / 2 / per_col) / align * align;
     if (cb < align) cb = align;
     if (cb >= C) cb = C;

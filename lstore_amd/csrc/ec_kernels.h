@@ -121,6 +121,9 @@ hipError_t launch_bitmatrix(const ApplyArgs &a, hipStream_t stream, int grid_blo
 bool bitmatrix_w_supported(int w);
 // matrix codes over GF(2^16) / GF(2^32) (a.w), little-endian words, R <= 8
 hipError_t launch_wordwise(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
+// Cauchy codes at w = 16 / 32 in the packet layout, bit-sliced over GF(2^w): the wordwise
+// image supplies the coefficients; R <= 8 per launch at w = 16, <= 4 at w = 32
+hipError_t launch_gfw_bitsliced(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
 // host helper: the w products c * x^b (b = 0..w-1) of a wordwise cell, replicated for w = 16
 void make_word_cell(uint32_t c, int w, uint32_t *out);
 

@@ -127,6 +127,18 @@ hipError_t launch_wordwise(const ApplyArgs &a, hipStream_t st, int grid_blocks) 
   return by_r(a.R, [&](auto r) { return dispatch_wordwise<decltype(r)::value>(a, st, grid); });
 }
 
+hipError_t launch_gfw_bitsliced(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
+  if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > (a.w == 32 ? 4 : 8) || (a.w != 16 && a.w != 32) || !a.masks ||
+      a.packet <= 0 || a.packet % 4 != 0 || a.size % (static_cast<int64_t>(a.w) * a.packet) != 0)
+    return hipErrorInvalidValue;
+  if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
+  const uint64_t col_bytes = a.size / a.w;
+  const uint64_t ntiles = ((col_bytes + kBlock * 4 - 1) / (kBlock * 4)) * static_cast<uint64_t>(a.nstripes);
+  if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
+  const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);
+  return by_r(a.R, [&](auto r) { return dispatch_gfw_bitsliced<decltype(r)::value>(a, st, grid); });
+}
+
 // ------------------------------------------------------------------ stripe magic (adler32)
 namespace {
 

@@ -657,6 +657,86 @@ __global__ __launch_bounds__(kBlock) void k_gfw_wordwise(ApplyArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ bit-sliced GF(2^16) / GF(2^32)
+// Cauchy codes at w = 16 / 32 in Jerasure's packet layout: a super-packet is W packets of P
+// bytes, and bit x of element (t, b) is bit b of byte t of packet x, so a 32-bit word of each
+// of the W packets holds bit x of 32 elements -- the w = 8 bit-sliced scheme with W slices.
+// Multiplying all 32 elements by x renames the slices and XORs the top slice into the
+// polynomial's taps (Jerasure's fields, galois.c:65-98: x^16 = x^12+x^3+x+1, x^32 =
+// x^22+x^2+x+1), and c*e = sum_{t: c_t = 1} x^t e.  Identical bytes to the bitmatrix of the
+// GF(2^W) coefficient matrix (what jerasure_bitmatrix_encode applies), in W XORs per set
+// coefficient bit instead of one per set bitmatrix bit, under R*W uniform branches per input
+// instead of R*W*W.  Coefficients come from the wordwise image (product b = 0 of a cell).
+template <int W>
+__device__ __forceinline__ void times_x_sliced(uint32_t (&e)[W]) {
+  const uint32_t top = e[W - 1];
+#pragma unroll
+  for (int i = W - 1; i > 0; --i) e[i] = e[i - 1];
+  e[0] = top;
+  if constexpr (W == 16) {
+    e[1] ^= top;
+    e[3] ^= top;
+    e[12] ^= top;
+  } else {
+    e[1] ^= top;
+    e[2] ^= top;
+    e[22] ^= top;
+  }
+}
+
+template <int R, int W>
+__global__ __launch_bounds__(kBlock) void k_gfw_bitsliced(ApplyArgs a) {
+  const int K = a.K;
+  const uint32_t P = static_cast<uint32_t>(a.packet);
+  const uint32_t col_bytes = static_cast<uint32_t>(a.size / W);  // nsuper * P
+  constexpr uint32_t kTile = kBlock * 4;
+  constexpr uint32_t kCoefMask = W == 16 ? 0xFFFFu : 0xFFFFFFFFu;
+  const uint32_t tiles_per_stripe = (col_bytes + kTile - 1) / kTile;
+  const uint32_t ntiles = tiles_per_stripe * static_cast<uint32_t>(a.nstripes);
+  ConstU32 *prod = reinterpret_cast<ConstU32 *>(reinterpret_cast<uintptr_t>(a.masks));
+  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+    const uint32_t s = t / tiles_per_stripe;
+    const uint32_t colb = (t - s * tiles_per_stripe) * kTile + threadIdx.x * 4;
+    if (colb >= col_bytes) continue;
+    const uint32_t sp = colb / P;
+    const int64_t off = static_cast<int64_t>(sp) * W * P + (colb - sp * P);
+    uint32_t acc[R][W];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int l = 0; l < W; ++l) acc[r][l] = 0u;
+    for (int j = 0; j < K; ++j) {
+      const uint64_t p = a.in[j].base + s * a.in[j].stride + off;
+      uint32_t e[W];
+#pragma unroll
+      for (int x = 0; x < W; ++x) e[x] = __builtin_nontemporal_load(gptr<uint32_t>(p + x * P));
+      uint32_t c[R], cm = 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        c[r] = prod[(r * K + j) * W] & kCoefMask;  // wave-uniform -> scalar loads
+        cm |= c[r];
+      }
+#pragma unroll
+      for (int b = 0; b < W; ++b) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if ((c[r] >> b) & 1u) {
+#pragma unroll
+            for (int x = 0; x < W; ++x) acc[r][x] ^= e[x];
+          }
+        if (b == W - 1 || (cm >> (b + 1)) == 0) break;
+        times_x_sliced<W>(e);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
+#pragma unroll
+      for (int l = 0; l < W; ++l) __builtin_nontemporal_store(acc[r][l], gptr_w<uint32_t>(q + l * P));
+    }
+  }
+}
+
 // word sizes the liberation family can produce: primes (liberation), p-1 for prime p
 // (blaum_roth), 8 (liber8tion); 16 and 32 for Cauchy at those word sizes
 #define LSEC_BITMATRIX_W(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(10) X(11) X(12) X(13) X(16) X(17) \
@@ -752,12 +832,27 @@ hipError_t dispatch_wordwise(const ApplyArgs &a, hipStream_t st, int grid) {
   return hipGetLastError();
 }
 
+// at most 8 rows per launch at w = 16, 4 at w = 32 (acc[R][W] lives in VGPRs)
+template <int R>
+hipError_t dispatch_gfw_bitsliced(const ApplyArgs &a, hipStream_t st, int grid) {
+  if (a.w == 16) {
+    hipLaunchKernelGGL((k_gfw_bitsliced<R, 16>), dim3(grid), dim3(kBlock), 0, st, a);
+  } else if constexpr (R <= 4) {
+    if (a.w != 32) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_gfw_bitsliced<R, 32>), dim3(grid), dim3(kBlock), 0, st, a);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 #define LSEC_DECLARE_R(RR)                                                                         \
   extern template hipError_t dispatch_bytewise<RR>(const ApplyArgs &, hipStream_t, int, int);      \
   extern template hipError_t dispatch_bitsliced<RR>(const ApplyArgs &, hipStream_t, int, int);         \
   extern template hipError_t dispatch_bitmatrix<RR>(const ApplyArgs &, hipStream_t, int);           \
   extern template hipError_t dispatch_bytewise_magic<RR>(const ApplyArgs &, hipStream_t, int);          \
-  extern template hipError_t dispatch_wordwise<RR>(const ApplyArgs &, hipStream_t, int);
+  extern template hipError_t dispatch_wordwise<RR>(const ApplyArgs &, hipStream_t, int);         \
+  extern template hipError_t dispatch_gfw_bitsliced<RR>(const ApplyArgs &, hipStream_t, int);
 #ifndef LSEC_INSTANTIATING
 LSEC_DECLARE_R(1) LSEC_DECLARE_R(2) LSEC_DECLARE_R(3) LSEC_DECLARE_R(4)
 LSEC_DECLARE_R(5) LSEC_DECLARE_R(6) LSEC_DECLARE_R(7) LSEC_DECLARE_R(8)

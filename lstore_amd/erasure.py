@@ -231,7 +231,8 @@ class Plan:
     @property
     def kernel(self) -> int:
         """1 = bytewise GF(2^8), 2 = bitsliced GF(2^8) (Cauchy), 3 = GF(2) bitmatrix (liberation
-        family, Cauchy at w = 16/32), 4 = wordwise GF(2^16/2^32) (RS), 0 = no GPU kernel"""
+        family), 4 = wordwise GF(2^16/2^32) (RS), 5 = bitsliced GF(2^16/2^32) (Cauchy at
+        w = 16/32), 0 = no GPU kernel"""
         return lib().lsec_plan_kernel(self._p)
 
     def matrix(self):

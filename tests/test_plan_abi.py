@@ -190,6 +190,6 @@ def test_unsupported_method_is_an_error_not_a_fallback(built):
         with L.Plan.new(L.REED_SOL_VAN, 0, 6, 3, w, 8, 8) as p:
             assert p.kernel == 4   # wordwise GF(2^w)
         with L.Plan.new(L.CAUCHY_GOOD, 0, 6, 3, w, 8, 8) as p:
-            assert p.kernel == 3   # generic bitmatrix
+            assert p.kernel == 5   # bit-sliced GF(2^w)
     with L.Plan.generate(6 * 7 * 64 * 4, L.LIBERATION, 6, 2) as p:
         assert p.kernel == 3   # generic bitmatrix kernel
