@@ -19,6 +19,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdarg>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -748,9 +749,35 @@ bool is_pinned_host(const void *ptr) {
 
 // every staged shard of the first and last stripe pinned?  (a stray pageable pointer in
 // between stays correct -- hipMemcpyAsync accepts pageable memory too, only slower)
+// Ranges pinned in place by a running call (InPlacePin), page-rounded.  Another call that
+// touches them must not take them for caller-pinned memory: the owner unregisters them when
+// it returns, maybe while the other call's DMA is still queued.
+std::mutex g_inplace_mu;
+std::vector<std::pair<uintptr_t, uintptr_t>> g_inplace;
+
+constexpr uintptr_t kPage = 4096;
+
+bool inplace_overlaps_locked(uintptr_t lo, uintptr_t hi) {
+  for (const auto &r : g_inplace)
+    if (lo < r.second && r.first < hi) return true;
+  return false;
+}
+
 bool pinned_layout(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids) {
   static const bool off = getenv("LSEC_NO_PINNED_DMA") != nullptr;
   if (off) return false;
+  {
+    std::lock_guard<std::mutex> lk(g_inplace_mu);
+    if (!g_inplace.empty()) {
+      for (int s = 0; s < nstripes; ++s) {
+        for (const std::vector<int> *ids : {&in_ids, &out_ids})
+          for (int id : *ids) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(ptrs[static_cast<size_t>(s) * km + id]) & ~(kPage - 1);
+            if (inplace_overlaps_locked(a, a + kPage)) return false;
+          }
+      }
+    }
+  }
   for (int s : {0, nstripes - 1}) {
     for (int id : in_ids)
       if (!is_pinned_host(ptrs[static_cast<size_t>(s) * km + id])) return false;
@@ -759,6 +786,87 @@ bool pinned_layout(char **ptrs, int nstripes, int km, const std::vector<int> &in
   }
   return true;
 }
+
+// Pageable caller buffers of a large batch are pinned in place for the duration of the call
+// when they form a few dense regions: hipHostRegister pins at 190-450 GB/s on the box
+// (tools/hostreg_probe.py) while packing copies at ~20 GB/s per thread, so the DMA engines
+// then read and write the caller's pages directly and the host cores stay idle.  Regions are
+// exactly the caller's chunks merged where they touch (LStore: a cache page of k data chunks,
+// a parity buffer), so no other buffer shares a registration.  Any failure (already
+// registered by another call, too many regions) keeps the packing path.
+class InPlacePin {
+ public:
+  ~InPlacePin() { release(); }
+  bool pin(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
+           long long C) {
+    static const bool off = getenv("LSEC_NO_HOST_REGISTER") != nullptr;
+    if (off) return false;
+    std::vector<std::pair<char *, char *>> pieces;
+    pieces.reserve(static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()));
+    for (int s = 0; s < nstripes; ++s) {
+      for (int id : in_ids) pieces.push_back({ptrs[static_cast<size_t>(s) * km + id], ptrs[static_cast<size_t>(s) * km + id] + C});
+      for (int id : out_ids) pieces.push_back({ptrs[static_cast<size_t>(s) * km + id], ptrs[static_cast<size_t>(s) * km + id] + C});
+    }
+    std::sort(pieces.begin(), pieces.end());
+    std::vector<std::pair<char *, char *>> regions;
+    for (const auto &pc : pieces) {
+      if (!regions.empty() && pc.first < regions.back().second) return false;  // overlapping chunks
+      if (!regions.empty() && pc.first == regions.back().second)
+        regions.back().second = pc.second;
+      else
+        regions.push_back(pc);
+      if (regions.size() > kMaxRegions) return false;
+    }
+    size_t total = 0;
+    for (const auto &r : regions) total += static_cast<size_t>(r.second - r.first);
+    if (total < kMinBytes) return false;  // packing a small batch is cheaper than the syscalls
+    {
+      // claim the page-rounded regions, so a concurrent call over the same pages packs
+      std::lock_guard<std::mutex> lk(g_inplace_mu);
+      for (const auto &r : regions) {
+        const uintptr_t lo = reinterpret_cast<uintptr_t>(r.first) & ~(kPage - 1);
+        const uintptr_t hi = (reinterpret_cast<uintptr_t>(r.second) + kPage - 1) & ~(kPage - 1);
+        if (inplace_overlaps_locked(lo, hi)) {
+          claimed_.clear();
+          return false;
+        }
+        claimed_.push_back({lo, hi});
+      }
+      for (size_t i = 1; i < claimed_.size(); ++i)
+        if (claimed_[i].first < claimed_[i - 1].second) {  // two (sorted) regions share a page
+          claimed_.clear();
+          return false;
+        }
+      g_inplace.insert(g_inplace.end(), claimed_.begin(), claimed_.end());
+    }
+    for (const auto &r : regions) {
+      if (hipHostRegister(r.first, static_cast<size_t>(r.second - r.first), hipHostRegisterPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        release();
+        return false;
+      }
+      held_.push_back(r.first);
+    }
+    return true;
+  }
+  void release() {
+    for (char *b : held_) (void)hipHostUnregister(b);
+    held_.clear();
+    if (claimed_.empty()) return;
+    std::lock_guard<std::mutex> lk(g_inplace_mu);
+    for (const auto &c : claimed_) {
+      auto it = std::find(g_inplace.begin(), g_inplace.end(), c);
+      if (it != g_inplace.end()) g_inplace.erase(it);
+    }
+    claimed_.clear();
+  }
+
+ private:
+  static constexpr size_t kMaxRegions = 1024;
+  static constexpr size_t kMinBytes = 8ull << 20;
+  std::vector<char *> held_;
+  std::vector<std::pair<uintptr_t, uintptr_t>> claimed_;
+};
 
 // DMA runs: pieces whose source and destination both continue the previous piece merge
 // into one copy (LStore's k data chunks of a stripe sit back to back in one cache page, so
@@ -836,8 +944,12 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
     dmagic = reinterpret_cast<uint8_t *>(dacc + 2ull * nstripes);
   }
 
-  // pinned callers: DMA straight between their buffers and the device slots
-  const bool pinned = pinned_layout(ptrs, nstripes, km, in_ids, out_ids);
+  // pinned callers (or pageable ones pinned in place for this call): DMA straight between
+  // their buffers and the device slots.  `inplace` is declared before the staging users, so
+  // its registrations outlive every DMA (all are drained before run_host returns).
+  InPlacePin inplace;
+  const bool pinned = pinned_layout(ptrs, nstripes, km, in_ids, out_ids) ||
+                      inplace.pin(ptrs, nstripes, km, in_ids, out_ids, C);
   std::vector<DmaRun> runs;
 
   auto unpack = [&](Staging::Slot &sl) -> int {

@@ -491,6 +491,52 @@ def test_host_path_pinned_buffers(cuda, method, k, m, size, n):
         assert np.array_equal(st[:, [1, k + 1]], keep)
 
 
+def test_pageable_batches_pinned_in_place_share_inputs(cuda):
+    """Large pageable batches are pinned in place (hipHostRegister) for the call.  Threads that
+    encode from the SAME data chunks at once (each into its own parity buffers) contend for
+    the registration: the loser packs instead, nobody DMAs from pages another call is about
+    to unregister, and every parity equals the oracle's."""
+    import threading
+
+    k, m, size, n = 6, 3, 1 << 20, 6  # 36 MiB of data: above the in-place threshold
+    data = np.random.default_rng(7).integers(0, 256, (n, k, size), dtype=np.uint8)
+    with L.Plan.for_chunk(L.REED_SOL_VAN, k, m, size) as p:
+        want = [O.encode(O.REED_SOL_VAN, data[s], m) for s in range(n)]
+        errors = []
+
+        def worker(t):
+            try:
+                par = np.zeros((n, m, size), np.uint8)
+                addrs = []
+                for s in range(n):
+                    addrs += [data[s, i].ctypes.data for i in range(k)]
+                    addrs += [par[s, j].ctypes.data for j in range(m)]
+                arr = p._ptr_array(addrs)
+                for it in range(4):
+                    par[:] = 0
+                    p.encode_stripes_ptrs(arr, n, size)
+                    for s in range(n):
+                        if not np.array_equal(par[s], want[s]):
+                            errors.append((t, it, s))
+            except Exception as e:  # noqa: BLE001
+                errors.append((t, repr(e)))
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errors, errors[:5]
+        # and a pageable decode of a batch whose chunks are one dense region per stripe
+        st = np.zeros((n, k + m, size), np.uint8)
+        st[:, :k] = data
+        p.encode_stripes(st)
+        full = st.copy()
+        st[:, [0, 4, k + 2]] = 0xA5
+        p.decode_stripes(st, [0, 4, k + 2])
+        assert np.array_equal(st, full)
+
+
 def test_fn_pointer_pinned_and_pageable_callers_coalesced(cuda):
     """Concurrent single-stripe calls, half on page-locked and half on pageable buffers, go
     through the dispatcher together; each gets its own parity and rebuilds."""
