@@ -467,7 +467,7 @@ int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
 // KBITMATRIX the uint32 row masks [(r*w+l)*K + j].
 int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in, const ShardRef *out,
                   int nstripes, long long size, int packet, hipStream_t st, int w = 8) {
-  const int rmax = kind == KBITMATRIX ? 2 : (kind == KBITSLICEDW && w == 32) ? 4 : 8;
+  const int rmax = kind == KBITMATRIX ? 2 : ((kind == KBITSLICEDW || kind == KWORDWISE) && w == 32) ? 4 : 8;
   for (int r0 = 0; r0 < R; r0 += rmax) {
     lsec::ApplyArgs a;
     std::memset(&a, 0, sizeof(a));

@@ -119,7 +119,8 @@ hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t stream, int grid_blo
 // w = 16 / 32): any w in LSEC_BITMATRIX_W, R <= 2 per launch
 hipError_t launch_bitmatrix(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
 bool bitmatrix_w_supported(int w);
-// matrix codes over GF(2^16) / GF(2^32) (a.w), little-endian words, R <= 8
+// matrix codes over GF(2^16) / GF(2^32) (a.w), little-endian words, R <= 8: bit-sliced after
+// an in-register transpose (R <= 4 at w = 32), per-bit masks beyond that
 hipError_t launch_wordwise(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
 // Cauchy codes at w = 16 / 32 in the packet layout, bit-sliced over GF(2^w): the wordwise
 // image supplies the coefficients; R <= 8 per launch at w = 16, <= 4 at w = 32

@@ -120,10 +120,15 @@ hipError_t launch_wordwise(const ApplyArgs &a, hipStream_t st, int grid_blocks) 
   if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > 8 || (a.w != 16 && a.w != 32) || !a.masks || a.size % 8 != 0)
     return hipErrorInvalidValue;
   if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
-  const uint64_t tile = kBlock * (a.w == 16 ? 16ull : 8ull);  // bytes per shard per tile (VW = 4 / 2 dwords per lane)
+  // transposed bit-sliced kernel (4*w bytes per lane) up to 8 rows at w = 16 and 4 at w = 32;
+  // the mask-per-bit kernel (16 / 8 bytes per lane) beyond that
+  // (lsec_set_kernel_variant's second argument 10 selects the mask-per-bit kernel: A/B runs)
+  const bool transposed = g_bs_variant != 10 && (a.w == 16 || a.R <= 4);
+  const uint64_t tile = kBlock * (transposed ? 4ull * a.w : a.w == 16 ? 16ull : 8ull);
   const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);
+  if (transposed) return by_r(a.R, [&](auto r) { return dispatch_gfw_transposed<decltype(r)::value>(a, st, grid); });
   return by_r(a.R, [&](auto r) { return dispatch_wordwise<decltype(r)::value>(a, st, grid); });
 }
 

@@ -737,6 +737,150 @@ __global__ __launch_bounds__(kBlock) void k_gfw_bitsliced(ApplyArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ transposed GF(2^16) / GF(2^32)
+// RS / r6 at w = 16 / 32 keep Jerasure's word layout (element t = little-endian uint16/uint32
+// at byte 2t / 4t, galois.c:527-604, :730-810).  Each lane loads W dwords of a shard (32
+// elements: W/4 coalesced 16 B pieces), transposes the W x W bit blocks in registers so that
+// word x holds bit x of all 32 elements, runs k_gfw_bitsliced's arithmetic (one XOR per slice
+// per set coefficient bit), and transposes back.  A W x W transpose is log2(W) swap stages:
+// byte and halfword stages are two v_perm_b32 per pair of words, bit stages two shifts and two
+// v_bfi_b32.  Elements never mix, so a zero-filled tail produces zeros that are not stored.
+template <int W, int d>
+__device__ __forceinline__ void transpose_bits(uint32_t (&D)[W], uint32_t m) {
+#pragma unroll
+  for (int r = 0; r < W; ++r) {
+    if (r & d) continue;
+    const uint32_t x = D[r], y = D[r + d];
+    D[r] = (x & m) | ((y << d) & ~m);
+    D[r + d] = ((x >> d) & m) | (y & ~m);
+  }
+}
+
+template <int W>
+__device__ __forceinline__ void transpose_units(uint32_t (&D)[W]) {
+  if constexpr (W == 32) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t x = D[r], y = D[r + 16];
+      D[r] = __builtin_amdgcn_perm(y, x, 0x05040100u);       // (x.lo, y.lo)
+      D[r + 16] = __builtin_amdgcn_perm(y, x, 0x07060302u);  // (x.hi, y.hi)
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < W; ++r) {
+    if (r & 8) continue;
+    const uint32_t x = D[r], y = D[r + 8];
+    D[r] = __builtin_amdgcn_perm(y, x, 0x06020400u);      // (x.b0, y.b0, x.b2, y.b2)
+    D[r + 8] = __builtin_amdgcn_perm(y, x, 0x07030501u);  // (x.b1, y.b1, x.b3, y.b3)
+  }
+  transpose_bits<W, 4>(D, 0x0F0F0F0Fu);
+  transpose_bits<W, 2>(D, 0x33333333u);
+  transpose_bits<W, 1>(D, 0x55555555u);
+}
+
+template <int R, int W, bool xor_only>
+__device__ __forceinline__ void gfw_transposed_tiles(const ApplyArgs &a) {
+  constexpr int kPieces = W / 4;  // 16 B pieces per lane per shard
+  constexpr uint32_t kTile = kBlock * 4 * W;
+  constexpr uint32_t kCoefMask = W == 16 ? 0xFFFFu : 0xFFFFFFFFu;
+  const int K = a.K;
+  const int64_t C = a.size;
+  const uint32_t tiles_per_stripe = static_cast<uint32_t>((C + kTile - 1) / kTile);
+  const uint32_t ntiles = tiles_per_stripe * static_cast<uint32_t>(a.nstripes);
+  ConstU32 *prod = reinterpret_cast<ConstU32 *>(reinterpret_cast<uintptr_t>(a.masks));
+  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+    const uint32_t s = t / tiles_per_stripe;
+    const int64_t base = static_cast<int64_t>(t - s * tiles_per_stripe) * kTile + threadIdx.x * 16;
+    if (base >= C) continue;
+    // whole tile in range: every piece is a full 16 B; otherwise per piece (C % 8 == 0)
+    const bool whole = static_cast<int64_t>(t - s * tiles_per_stripe) * kTile + kTile <= C;
+    uint32_t acc[R][W];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int l = 0; l < W; ++l) acc[r][l] = 0u;
+    for (int j = 0; j < K; ++j) {
+      const uint64_t p = a.in[j].base + s * a.in[j].stride;
+      uint32_t e[W];
+#pragma unroll
+      for (int q = 0; q < kPieces; ++q) {
+        const int64_t o = base + static_cast<int64_t>(q) * kBlock * 16;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (whole || o + 16 <= C) {
+          v = __builtin_nontemporal_load(gptr<u32x4>(p + o));
+        } else if (o + 8 <= C) {
+          const u32x2 h = *gptr<u32x2>(p + o);
+          v.x = h.x;
+          v.y = h.y;
+        }
+        e[4 * q] = v.x;
+        e[4 * q + 1] = v.y;
+        e[4 * q + 2] = v.z;
+        e[4 * q + 3] = v.w;
+      }
+      uint32_t c[R], cm = 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        c[r] = prod[(r * K + j) * W] & kCoefMask;  // wave-uniform -> scalar loads
+        cm |= c[r];
+      }
+      if (cm == 0) continue;
+      if constexpr (xor_only) {  // coefficients 0 / 1: plain XOR, no transposes
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if (c[r])
+#pragma unroll
+            for (int x = 0; x < W; ++x) acc[r][x] ^= e[x];
+        continue;
+      }
+      transpose_units<W>(e);
+#pragma unroll
+      for (int b = 0; b < W; ++b) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if ((c[r] >> b) & 1u) {
+#pragma unroll
+            for (int x = 0; x < W; ++x) acc[r][x] ^= e[x];
+          }
+        if (b == W - 1 || (cm >> (b + 1)) == 0) break;
+        times_x_sliced<W>(e);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if constexpr (!xor_only) transpose_units<W>(acc[r]);
+      const uint64_t q0 = a.out[r].base + s * a.out[r].stride;
+#pragma unroll
+      for (int q = 0; q < kPieces; ++q) {
+        const int64_t o = base + static_cast<int64_t>(q) * kBlock * 16;
+        const u32x4 v = {acc[r][4 * q], acc[r][4 * q + 1], acc[r][4 * q + 2], acc[r][4 * q + 3]};
+        if (whole || o + 16 <= C) {
+          __builtin_nontemporal_store(v, gptr_w<u32x4>(q0 + o));
+        } else if (o + 8 <= C) {
+          u32x2 h;
+          h.x = v.x;
+          h.y = v.y;
+          *gptr_w<u32x2>(q0 + o) = h;
+        }
+      }
+    }
+  }
+}
+
+// One kernel, two whole tile loops chosen by a uniform branch: a launch whose coefficients are
+// all 0 / 1 (XOR-of-survivors decodes) is plain XOR and skips the bit slicing.
+template <int R, int W>
+__global__ __launch_bounds__(kBlock) void k_gfw_transposed(ApplyArgs a) {
+  constexpr uint32_t kCoefMask = W == 16 ? 0xFFFFu : 0xFFFFFFFFu;
+  ConstU32 *prod = reinterpret_cast<ConstU32 *>(reinterpret_cast<uintptr_t>(a.masks));
+  bool xor_only = true;
+  for (int i = 0; i < R * a.K && xor_only; ++i) xor_only = (prod[i * W] & kCoefMask) <= 1u;
+  if (xor_only)
+    gfw_transposed_tiles<R, W, true>(a);
+  else
+    gfw_transposed_tiles<R, W, false>(a);
+}
+
 // word sizes the liberation family can produce: primes (liberation), p-1 for prime p
 // (blaum_roth), 8 (liber8tion); 16 and 32 for Cauchy at those word sizes
 #define LSEC_BITMATRIX_W(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(10) X(11) X(12) X(13) X(16) X(17) \
@@ -834,6 +978,19 @@ hipError_t dispatch_wordwise(const ApplyArgs &a, hipStream_t st, int grid) {
 
 // at most 8 rows per launch at w = 16, 4 at w = 32 (acc[R][W] lives in VGPRs)
 template <int R>
+hipError_t dispatch_gfw_transposed(const ApplyArgs &a, hipStream_t st, int grid) {
+  if (a.w == 16) {
+    hipLaunchKernelGGL((k_gfw_transposed<R, 16>), dim3(grid), dim3(kBlock), 0, st, a);
+  } else if constexpr (R <= 4) {
+    if (a.w != 32) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_gfw_transposed<R, 32>), dim3(grid), dim3(kBlock), 0, st, a);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+template <int R>
 hipError_t dispatch_gfw_bitsliced(const ApplyArgs &a, hipStream_t st, int grid) {
   if (a.w == 16) {
     hipLaunchKernelGGL((k_gfw_bitsliced<R, 16>), dim3(grid), dim3(kBlock), 0, st, a);
@@ -852,7 +1009,8 @@ hipError_t dispatch_gfw_bitsliced(const ApplyArgs &a, hipStream_t st, int grid) 
   extern template hipError_t dispatch_bitmatrix<RR>(const ApplyArgs &, hipStream_t, int);           \
   extern template hipError_t dispatch_bytewise_magic<RR>(const ApplyArgs &, hipStream_t, int);          \
   extern template hipError_t dispatch_wordwise<RR>(const ApplyArgs &, hipStream_t, int);         \
-  extern template hipError_t dispatch_gfw_bitsliced<RR>(const ApplyArgs &, hipStream_t, int);
+  extern template hipError_t dispatch_gfw_bitsliced<RR>(const ApplyArgs &, hipStream_t, int);      \
+  extern template hipError_t dispatch_gfw_transposed<RR>(const ApplyArgs &, hipStream_t, int);
 #ifndef LSEC_INSTANTIATING
 LSEC_DECLARE_R(1) LSEC_DECLARE_R(2) LSEC_DECLARE_R(3) LSEC_DECLARE_R(4)
 LSEC_DECLARE_R(5) LSEC_DECLARE_R(6) LSEC_DECLARE_R(7) LSEC_DECLARE_R(8)

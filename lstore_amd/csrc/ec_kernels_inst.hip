@@ -14,4 +14,5 @@ template hipError_t dispatch_bitmatrix<LSEC_R>(const ApplyArgs &, hipStream_t, i
 template hipError_t dispatch_bytewise_magic<LSEC_R>(const ApplyArgs &, hipStream_t, int);
 template hipError_t dispatch_wordwise<LSEC_R>(const ApplyArgs &, hipStream_t, int);
 template hipError_t dispatch_gfw_bitsliced<LSEC_R>(const ApplyArgs &, hipStream_t, int);
+template hipError_t dispatch_gfw_transposed<LSEC_R>(const ApplyArgs &, hipStream_t, int);
 }  // namespace lsec

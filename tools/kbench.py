@@ -26,9 +26,12 @@ CONFIGS = {
     "rs124": (L.REED_SOL_VAN, 12, 4, 1 << 20),
     "rs84": (L.REED_SOL_VAN, 8, 4, 1 << 20),
     "cg206": (L.CAUCHY_GOOD, 20, 6, 256 << 10),
-    # wide fields (w = 16 / 32): wordwise RS, bitmatrix Cauchy
+    # wide fields (w = 16 / 32): transposed bit-sliced RS, bit-sliced Cauchy
     "rs63w16": (L.REED_SOL_VAN, 6, 3, 1 << 20, 16),
     "rs63w32": (L.REED_SOL_VAN, 6, 3, 1 << 20, 32),
+    "rs104w16": (L.REED_SOL_VAN, 10, 4, 1 << 20, 16),
+    "rs104w32": (L.REED_SOL_VAN, 10, 4, 1 << 20, 32),
+    "rs206w16": (L.REED_SOL_VAN, 20, 6, 256 << 10, 16),
     "cg63w16": (L.CAUCHY_GOOD, 6, 3, 1 << 20, 16),
     "cg63w32": (L.CAUCHY_GOOD, 6, 3, 1 << 20, 32),
 }
