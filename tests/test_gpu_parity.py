@@ -82,7 +82,9 @@ def test_liberation_family_vs_reference(cuda, method, k, w):
     (L.REED_SOL_VAN, 6, 3, 16, 4104, 0),      # 4104 % 16 == 8: ragged last lane
     (L.REED_SOL_VAN, 10, 4, 32, 8200, 0),
     (L.REED_SOL_VAN, 20, 6, 16, 65536, 0),
-    (L.REED_SOL_VAN, 12, 9, 32, 4096, 0),     # R = 9 > 8: two launches
+    (L.REED_SOL_VAN, 12, 9, 32, 4096, 0),     # R = 9: launches of 4 + 4 + 1 rows at w = 32
+    (L.REED_SOL_VAN, 4, 2, 16, 2 * 16384 + 8, 0),   # 3 transposed tiles, last one 8 bytes long
+    (L.REED_SOL_VAN, 5, 3, 32, 3 * 32768 + 4104, 0),  # 4 tiles, last one ragged inside a lane
     (L.REED_SOL_R6_OP, 6, 2, 16, 2056, 0),
     (L.REED_SOL_R6_OP, 9, 2, 32, 4096, 0),
     (L.CAUCHY_GOOD, 6, 3, 16, 16 * 64 * 3, 64),
@@ -90,8 +92,8 @@ def test_liberation_family_vs_reference(cuda, method, k, w):
     (L.CAUCHY_GOOD, 10, 4, 32, 32 * 32 * 4, 32),
 ])
 def test_wide_fields_vs_oracle(cuda, method, k, m, w, size, P):
-    """RS / r6 over GF(2^16) / GF(2^32) (wordwise kernel, little-endian words) and Cauchy at
-    w = 16 / 32 (GF(2) bitmatrix kernel): encode and every single + some double/triple
+    """RS / r6 over GF(2^16) / GF(2^32) (transposed bit-sliced kernel, little-endian words) and
+    Cauchy at w = 16 / 32 (bit-sliced packet kernel): encode and every single + some double/triple
     erasure decodes, bit-exact vs the oracle restatement (pinned to the reference fixtures)."""
     import torch
 
