@@ -68,6 +68,7 @@ constexpr int kMaxM = 64;  // parity devices per stripe (output shard tables bel
 
 struct DecodeEntry {
   lsec::gf8::DecodePlan dp;
+  bool xor_only = false;  // GF(2^8) rows of 0 / 1 only (XOR of survivors)
   std::map<int, CoefCell *> dev_cells;  // device -> e x k cells
   std::vector<uint32_t> masks;          // bitmatrix codes: (e*w) x k row masks; wordwise: e x k x w products
   std::map<int, uint32_t *> dev_masks;
@@ -417,6 +418,7 @@ int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, con
     } else {
       const int m = static_cast<int>(e->impl->coding.size()) / k;
       if (!lsec::gf8::make_decode(k, m, e->impl->coding, ids, ent.dp)) return fail("decoding matrix is singular");
+      ent.xor_only = std::all_of(ent.dp.rows.begin(), ent.dp.rows.end(), [](int c) { return c == 0 || c == 1; });
     }
     it = e->impl->decode_cache.emplace(ids, std::move(ent)).first;
   }
@@ -443,6 +445,14 @@ int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, con
   *out = &ent;
   *cells = dc->second;
   return 0;
+}
+
+// A decode that only XORs survivors (a lost data shard rebuilt from P0, whose Cauchy-good /
+// RS row is all ones) is layout-agnostic, so Cauchy w = 8 packets go through the bytewise
+// kernel's plain-XOR path (same cells) instead of the bit-sliced one.
+int decode_kind(const PlanExt *e, const DecodeEntry *ent) {
+  const int kind = kernel_kind(e->pub.method, e->pub.w);
+  return kind == KBITSLICED && ent->xor_only ? KBYTEWISE : kind;
 }
 
 int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
@@ -542,7 +552,7 @@ int decode_dev(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C, co
     const lsec_shard_t &s = sh[ent->dp.erased[r]];
     out[r] = {reinterpret_cast<uint64_t>(s.base), s.stride};
   }
-  return enqueue_apply(kernel_kind(p->method, p->w), cells, k, R, in, out, nstripes, C, p->packet_size, st, p->w);
+  return enqueue_apply(decode_kind(e, ent), cells, k, R, in, out, nstripes, C, p->packet_size, st, p->w);
 }
 
 // ---------------------------------------------------------------- host copy pool
@@ -1494,7 +1504,7 @@ int decode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C, cons
     const void *cells = nullptr;
     if (decode_entry(e, ids, &ent, &cells)) return -1;
     return run_host_auto(e, ptrs + static_cast<size_t>(s0) * km, n, C, ent->dp.survivors, ent->dp.erased, cells,
-                         kernel_kind(p->method, p->w));
+                         decode_kind(e, ent));
   });
 }
 
