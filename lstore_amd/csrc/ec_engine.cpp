@@ -410,6 +410,8 @@ int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, con
       ent.dp.survivors = wp.survivors;
       ent.dp.erased = wp.erased;
       ent.masks = word_image(wp.rows, static_cast<int>(wp.erased.size()), k, w);
+      ent.xor_only = std::all_of(wp.rows.begin(), wp.rows.end(), [](uint32_t c) { return c <= 1u; });
+      if (ent.xor_only) ent.dp.rows.assign(wp.rows.begin(), wp.rows.end());  // 0 / 1 as GF(2^8) cells
     } else if (kind == KBITMATRIX) {
       const lio_erasure_plan_t *p = &e->pub;
       std::vector<int> bm(p->encode_bitmatrix, p->encode_bitmatrix + static_cast<size_t>(k) * p->parity_strips * p->w * p->w);
@@ -423,7 +425,7 @@ int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, con
     it = e->impl->decode_cache.emplace(ids, std::move(ent)).first;
   }
   DecodeEntry &ent = it->second;
-  if (bitm) {
+  if (bitm && !ent.xor_only) {
     auto dm = ent.dev_masks.find(dev);
     if (dm == ent.dev_masks.end()) {
       uint32_t *d = nullptr;
@@ -448,11 +450,12 @@ int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, con
 }
 
 // A decode that only XORs survivors (a lost data shard rebuilt from P0, whose Cauchy-good /
-// RS row is all ones) is layout-agnostic, so Cauchy w = 8 packets go through the bytewise
-// kernel's plain-XOR path (same cells) instead of the bit-sliced one.
+// RS row is all ones) is layout- and field-agnostic, so Cauchy packets and GF(2^16) / GF(2^32)
+// words go through the bytewise kernel's plain-XOR path (0 / 1 cells) instead.
 int decode_kind(const PlanExt *e, const DecodeEntry *ent) {
   const int kind = kernel_kind(e->pub.method, e->pub.w);
-  return kind == KBITSLICED && ent->xor_only ? KBYTEWISE : kind;
+  const bool field = kind == KBITSLICED || kind == KWORDWISE || kind == KBITSLICEDW;
+  return field && ent->xor_only ? KBYTEWISE : kind;
 }
 
 int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
@@ -776,16 +779,16 @@ bool inplace_overlaps_locked(uintptr_t lo, uintptr_t hi) {
 bool pinned_layout(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids) {
   static const bool off = getenv("LSEC_NO_PINNED_DMA") != nullptr;
   if (off) return false;
-  {
-    std::lock_guard<std::mutex> lk(g_inplace_mu);
-    if (!g_inplace.empty()) {
-      for (int s = 0; s < nstripes; ++s) {
-        for (const std::vector<int> *ids : {&in_ids, &out_ids})
-          for (int id : *ids) {
-            const uintptr_t a = reinterpret_cast<uintptr_t>(ptrs[static_cast<size_t>(s) * km + id]) & ~(kPage - 1);
-            if (inplace_overlaps_locked(a, a + kPage)) return false;
-          }
-      }
+  // held across the attribute queries too: a registration claimed after the overlap scan
+  // must not be seen as caller-pinned
+  std::lock_guard<std::mutex> lk(g_inplace_mu);
+  if (!g_inplace.empty()) {
+    for (int s = 0; s < nstripes; ++s) {
+      for (const std::vector<int> *ids : {&in_ids, &out_ids})
+        for (int id : *ids) {
+          const uintptr_t a = reinterpret_cast<uintptr_t>(ptrs[static_cast<size_t>(s) * km + id]) & ~(kPage - 1);
+          if (inplace_overlaps_locked(a, a + kPage)) return false;
+        }
     }
   }
   for (int s : {0, nstripes - 1}) {
@@ -830,6 +833,21 @@ class InPlacePin {
     size_t total = 0;
     for (const auto &r : regions) total += static_cast<size_t>(r.second - r.first);
     if (total < kMinBytes) return false;  // packing a small batch is cheaper than the syscalls
+    // Each DMA from registered pageable memory costs ~50 us on top of the bytes (measured:
+    // 1 MB runs move at 14 GiB/s, 40 MB runs at 48), so pin only when the copies the pinned
+    // path will issue (one per run of host-contiguous chunks, stripe by stripe) average
+    // >= 4 MiB; smaller runs pack faster (profiles/r01_v20_sweep_c5.jsonl).
+    size_t runs = 0;
+    for (const std::vector<int> *ids : {&in_ids, &out_ids}) {
+      const char *end = nullptr;
+      for (int s = 0; s < nstripes; ++s)
+        for (int id : *ids) {
+          const char *b = ptrs[static_cast<size_t>(s) * km + id];
+          if (b != end) ++runs;
+          end = b + C;
+        }
+    }
+    if (runs == 0 || total / runs < kMinRun) return false;
     {
       // claim the page-rounded regions, so a concurrent call over the same pages packs
       std::lock_guard<std::mutex> lk(g_inplace_mu);
@@ -874,6 +892,7 @@ class InPlacePin {
  private:
   static constexpr size_t kMaxRegions = 1024;
   static constexpr size_t kMinBytes = 8ull << 20;
+  static constexpr size_t kMinRun = 4ull << 20;
   std::vector<char *> held_;
   std::vector<std::pair<uintptr_t, uintptr_t>> claimed_;
 };
