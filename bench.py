@@ -21,6 +21,8 @@ Also reported (same JSON line):
   cpu_baseline  the reference CPU path (oracle/_ref: vendor/jerasure via the plan dispatch)
                 on a bounded sample of the same workload, on this box's host cores
   host_path     PCIe-inclusive rate of et_encode_stripes / et_decode_stripes from host memory
+  hbm_copy_ref  this box's device-to-device copy rate (the practical HBM ceiling) and the
+                encode / decode kernels' rates relative to it
 Every run checks parity bit-exactly against the CPU oracle on sampled stripes.
 """
 import argparse
@@ -57,6 +59,7 @@ def parse():
     ap.add_argument("--pad", type=int, default=1024,
                     help="bytes left unused after every shard row in HBM (0 = shards exactly C apart)")
     ap.add_argument("--no-layout-ab", action="store_true", help="skip the unpadded-layout comparison")
+    ap.add_argument("--no-copy-ref", action="store_true", help="skip the device-copy HBM reference")
     return ap.parse_args()
 
 
@@ -295,6 +298,39 @@ def main():
                               "padded_value_from_launch_times": round(data_bytes / (t_enc + t_dec) / 2**30, 2)}
         del enc0, dec0
         torch.cuda.empty_cache()
+    copy_ref = None
+    if world == 1 and not a.no_copy_ref:
+        # the box's practical HBM ceiling beside the spec peak: streaming device copies of the
+        # encode launch's byte count (half read, half written), HIP events on the launch stream --
+        # the engine's probe kernel (lsec_hbm_copy_dev: the coding kernels' memory shape) and torch's copy_
+        data = par = rebuilt = None
+        torch.cuda.empty_cache()
+        nb = enc_hbm // 2
+        src = torch.empty(nb, dtype=torch.uint8, device=dev)
+        dst = torch.empty_like(src)
+
+        def probe():
+            if lib.lsec_hbm_copy_dev(dst.data_ptr(), src.data_ptr(), nb, sh):
+                raise E.ErasureError(E.last_error())
+
+        def timed(fn):
+            fn()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record(stream)
+            for _ in range(reps):
+                fn()
+            ev[1].record(stream)
+            torch.cuda.synchronize()
+            return ev[0].elapsed_time(ev[1]) / 1e3 / reps
+
+        t_probe, t_torch = timed(probe), timed(lambda: dst.copy_(src))
+        copy_ref = {"what": "device->device copy of (k+m)*C*N/2 bytes, read+write counted",
+                    "probe_GBps": round(2 * nb / t_probe / 1e9, 1), "probe_frac": round(2 * nb / t_probe / HBM_PEAK, 4),
+                    "torch_copy_GBps": round(2 * nb / t_torch / 1e9, 1),
+                    "encode_vs_probe": round((enc_hbm / t_enc) / (2 * nb / t_probe), 3),
+                    "decode_vs_probe": round((dec_hbm / t_dec) / (2 * nb / t_probe), 3)}
+        del src, dst
+        torch.cuda.empty_cache()
     if a.total_stripes > 0:
         value = k * C * a.total_stripes * a.steps / elapsed / 2**30
     else:
@@ -340,6 +376,7 @@ def main():
                          "decode_achieved_GBps": round(dec_hbm / t_dec / 1e9, 1),
                          "decode_frac": round(dec_hbm / t_dec / HBM_PEAK, 4)},
             "layout": layout,
+            "hbm_copy_ref": copy_ref,
             "cpu_baseline": cpu,
             "host_path": host,
             "parity_check": "bit-exact vs oracle on stripes %s" % pick,

@@ -212,6 +212,10 @@ const char *lsec_last_error(void);           /* thread-local message of the last
  * 0 = no GPU kernel (calls fail with -1) */
 int lsec_plan_kernel(lio_erasure_plan_t *plan);
 void lsec_set_kernel_variant(int bytewise_variant, int bitsliced_variant);  /* tuning experiments */
+/* Measurement probe, not part of the coding path: enqueue a streaming device copy dst <- src
+ * (bytes a multiple of 16, 16-byte aligned device pointers) on `stream` with the coding kernels'
+ * memory shape; bench.py times it as the box's practical HBM ceiling.  0 / -1. */
+int lsec_hbm_copy_dev(void *dst, const void *src, unsigned long long bytes, void *stream);
 
 #ifdef __cplusplus
 }

@@ -2256,4 +2256,10 @@ void lsec_set_kernel_variant(int bytewise_variant, int bitsliced_variant) {
   lsec::set_kernel_variant(bytewise_variant, bitsliced_variant);
 }
 
+int lsec_hbm_copy_dev(void *dst, const void *src, unsigned long long bytes, void *stream) {
+  const hipError_t e = lsec::launch_hbm_copy(dst, src, bytes, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return fail("lsec_hbm_copy_dev: %s", hipGetErrorString(e));
+  return 0;
+}
+
 }  // extern "C"

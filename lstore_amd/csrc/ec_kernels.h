@@ -107,6 +107,9 @@ struct GatherPiece {
 };
 hipError_t launch_gather(const GatherPiece *list, int n, char *dst, hipStream_t stream);
 
+// HBM probe (measurement only): dst <- src, bytes a multiple of 16, both 16-byte aligned.
+hipError_t launch_hbm_copy(void *dst, const void *src, uint64_t bytes, hipStream_t stream);
+
 // Host helper: fill one cell for coefficient c.
 void make_cell(uint8_t c, CoefCell &cell);
 

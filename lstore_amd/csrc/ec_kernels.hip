@@ -234,7 +234,40 @@ __global__ __launch_bounds__(kBlock) void k_gather(const GatherPiece *list, char
   for (uint64_t i = threadIdx.x; i < g.bytes / 8; i += kBlock) out[i] = __builtin_nontemporal_load(src + i);
 }
 
+// HBM probe: a plain streaming copy with the coding kernels' memory shape (one 8 KiB tile
+// per block, XCD-contiguous block order, 2 x 16 B non-temporal loads and stores per lane).
+// bench.py times it beside the encode as this box's practical read+write ceiling.
+__global__ __launch_bounds__(kBlock) void k_hbm_copy(uint64_t dst, uint64_t src, uint64_t n16) {
+  constexpr int kIt = 2;
+  const uint64_t ntiles = (n16 + kBlock * kIt - 1) / (kBlock * kIt);
+  for (uint64_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+    const uint64_t i0 = t * kBlock * kIt + threadIdx.x;
+    u32x4 v[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const uint64_t i = i0 + it * kBlock;
+      if (i < n16) v[it] = __builtin_nontemporal_load(gptr<u32x4>(src + i * 16));
+    }
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const uint64_t i = i0 + it * kBlock;
+      if (i < n16) __builtin_nontemporal_store(v[it], gptr_w<u32x4>(dst + i * 16));
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_hbm_copy(void *dst, const void *src, uint64_t bytes, hipStream_t st) {
+  if (!dst || !src || bytes % 16 != 0 || (reinterpret_cast<uint64_t>(dst) | reinterpret_cast<uint64_t>(src)) % 16)
+    return hipErrorInvalidValue;
+  const uint64_t n16 = bytes / 16, ntiles = (n16 + kBlock * 2 - 1) / (kBlock * 2);
+  if (ntiles == 0) return hipSuccess;
+  if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_hbm_copy, dim3(default_grid(ntiles)), dim3(kBlock), 0, st, reinterpret_cast<uint64_t>(dst),
+                     reinterpret_cast<uint64_t>(src), n16);
+  return hipGetLastError();
+}
 
 hipError_t launch_gather(const GatherPiece *list, int n, char *dst, hipStream_t st) {
   if (n <= 0) return hipSuccess;

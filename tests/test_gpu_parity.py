@@ -705,3 +705,24 @@ def test_concurrent_fn_pointer_calls(cuda):
         for th in threads:
             th.join()
         assert not errors, errors
+
+
+def test_hbm_copy_probe(cuda):
+    """lsec_hbm_copy_dev (bench.py's HBM ceiling probe) copies exactly, ragged tails included,
+    and refuses misaligned or non-16-multiple sizes."""
+    import torch
+
+    from lstore_amd import erasure as E
+
+    lib = E.lib()
+    st = torch.cuda.current_stream().cuda_stream
+    for n in (0, 16, 8192, 8192 + 48, (3 << 20) + 16 * 7):
+        src = torch.randint(0, 256, (n + 16,), dtype=torch.uint8, device=cuda)
+        dst = torch.zeros(n + 16, dtype=torch.uint8, device=cuda)
+        assert lib.lsec_hbm_copy_dev(dst.data_ptr(), src.data_ptr(), n, st) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(dst[:n], src[:n])
+        assert not dst[n:].any()
+    buf = torch.zeros(64, dtype=torch.uint8, device=cuda)
+    assert lib.lsec_hbm_copy_dev(buf.data_ptr(), buf.data_ptr() + 32, 24, st) == -1
+    assert lib.lsec_hbm_copy_dev(buf.data_ptr() + 8, buf.data_ptr() + 32, 16, st) == -1
