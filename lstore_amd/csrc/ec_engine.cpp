@@ -674,9 +674,13 @@ struct Staging {
     char **ptrs = nullptr;
     int s0 = 0, nb = 0;
     long long c0 = 0, clen = 0;  // column block of each shard this slot carries
+    // kernel transport (small host runs pinned in place): the slot's copy pieces, page-locked
+    lsec::CopyPiece *pl = nullptr;
+    size_t pl_cap = 0;
   } slot[kSlots];
   ~Staging() {
     for (auto &s : slot) {
+      if (s.pl) (void)hipHostFree(s.pl);
       if (s.d) (void)hipFree(s.d);
       if (s.h) (void)hipHostFree(s.h);
       if (s.done) (void)hipEventDestroy(s.done);
@@ -810,8 +814,10 @@ bool pinned_layout(char **ptrs, int nstripes, int km, const std::vector<int> &in
 class InPlacePin {
  public:
   ~InPlacePin() { release(); }
+  // kernel_ok: the caller can move small runs by kernel (lsec::launch_copy_pieces), so runs
+  // below kMinRun are worth pinning too; small_runs() then tells it to do so
   bool pin(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
-           long long C) {
+           long long C, bool kernel_ok) {
     static const bool off = getenv("LSEC_NO_HOST_REGISTER") != nullptr;
     if (off) return false;
     std::vector<std::pair<char *, char *>> pieces;
@@ -847,7 +853,9 @@ class InPlacePin {
           end = b + C;
         }
     }
-    if (runs == 0 || total / runs < kMinRun) return false;
+    if (runs == 0) return false;
+    small_runs_ = total / runs < kMinRun;
+    if (small_runs_ && !kernel_ok) return false;
     {
       // claim the page-rounded regions, so a concurrent call over the same pages packs
       std::lock_guard<std::mutex> lk(g_inplace_mu);
@@ -868,18 +876,36 @@ class InPlacePin {
       g_inplace.insert(g_inplace.end(), claimed_.begin(), claimed_.end());
     }
     for (const auto &r : regions) {
-      if (hipHostRegister(r.first, static_cast<size_t>(r.second - r.first), hipHostRegisterPortable) != hipSuccess) {
+      if (hipHostRegister(r.first, static_cast<size_t>(r.second - r.first), hipHostRegisterPortable | hipHostRegisterMapped) !=
+          hipSuccess) {
         (void)hipGetLastError();
         release();
         return false;
       }
       held_.push_back(r.first);
+      void *d = nullptr;
+      if (small_runs_ && (hipHostGetDevicePointer(&d, r.first, 0) != hipSuccess || !d)) {
+        (void)hipGetLastError();
+        release();
+        return false;
+      }
+      alias_.push_back({r.first, r.second, reinterpret_cast<intptr_t>(d) - reinterpret_cast<intptr_t>(r.first)});
     }
     return true;
+  }
+  bool small_runs() const { return !held_.empty() && small_runs_; }
+  // device address of host byte p inside a pinned region (regions are sorted and disjoint)
+  uint64_t alias(const char *p) const {
+    auto it = std::upper_bound(alias_.begin(), alias_.end(), p,
+                               [](const char *q, const Alias &a) { return q < a.lo; });
+    if (it == alias_.begin()) return 0;
+    --it;
+    return p < it->hi ? static_cast<uint64_t>(reinterpret_cast<intptr_t>(p) + it->delta) : 0;
   }
   void release() {
     for (char *b : held_) (void)hipHostUnregister(b);
     held_.clear();
+    alias_.clear();
     if (claimed_.empty()) return;
     std::lock_guard<std::mutex> lk(g_inplace_mu);
     for (const auto &c : claimed_) {
@@ -893,6 +919,12 @@ class InPlacePin {
   static constexpr size_t kMaxRegions = 1024;
   static constexpr size_t kMinBytes = 8ull << 20;
   static constexpr size_t kMinRun = 4ull << 20;
+  struct Alias {
+    const char *lo, *hi;
+    intptr_t delta;
+  };
+  bool small_runs_ = false;
+  std::vector<Alias> alias_;
   std::vector<char *> held_;
   std::vector<std::pair<uintptr_t, uintptr_t>> claimed_;
 };
@@ -911,6 +943,31 @@ void add_run(std::vector<DmaRun> &v, char *dst, const char *src, size_t n) {
     v.back().bytes += n;
   else
     v.push_back({dst, src, n});
+}
+
+// kernel transport pieces of one chunk (addresses already device-visible)
+// (returns 0 when either address is 0 -- a host byte outside the pinned regions -- so the
+// caller stops before launching)
+size_t add_pieces(lsec::CopyPiece *pl, size_t n, uint64_t src, uint64_t dst, size_t len) {
+  if (src == 0 || dst == 0) return 0;
+  for (size_t o = 0; o < len; o += lsec::kPieceBytes) pl[n++] = {src + o, dst + o, std::min<uint64_t>(lsec::kPieceBytes, len - o)};
+  return n;
+}
+
+// Opt-in (LSEC_KERNEL_COPY=1, read per call): large pageable batches of small host runs are
+// pinned in place and moved by kernel over their device aliases instead of being packed.
+// Needs every transferred chunk (and column block) 16-byte aligned.  Not the default: on the
+// box it held 29-32 GiB/s encode / 36-41 decode for C = 64-512 KiB whatever the host cores
+// did, while packing ran 23-38 / 28-45 depending on them (profiles/r01_v27_kernel_copy_ab.txt).
+bool kernel_transport_ok(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids,
+                         const std::vector<int> &out_ids, long long C, long long cb) {
+  const char *on = getenv("LSEC_KERNEL_COPY");
+  if (!on || *on != '1' || C % 16 != 0 || cb % 16 != 0) return false;
+  for (int s = 0; s < nstripes; ++s)
+    for (const std::vector<int> *ids : {&in_ids, &out_ids})
+      for (int id : *ids)
+        if (reinterpret_cast<uintptr_t>(ptrs[static_cast<size_t>(s) * km + id]) % 16 != 0) return false;
+  return true;
 }
 
 hipError_t issue_runs(const std::vector<DmaRun> &v, hipMemcpyKind kind, hipStream_t st) {
@@ -977,8 +1034,13 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   // their buffers and the device slots.  `inplace` is declared before the staging users, so
   // its registrations outlive every DMA (all are drained before run_host returns).
   InPlacePin inplace;
+  const bool kernel_ok = kernel_transport_ok(ptrs, nstripes, km, in_ids, out_ids, C, cb);
   const bool pinned = pinned_layout(ptrs, nstripes, km, in_ids, out_ids) ||
-                      inplace.pin(ptrs, nstripes, km, in_ids, out_ids, C);
+                      inplace.pin(ptrs, nstripes, km, in_ids, out_ids, C, kernel_ok);
+  // small host runs pinned in place move by kernel over their device aliases: one launch per
+  // direction instead of a DMA per run (each DMA from registered pageable memory costs ~50 us;
+  // 256 KiB runs move at 18 GB/s by DMA, 54 GB/s by one kernel: profiles/r01_v27_zerocopy_probe.txt)
+  const bool by_kernel = inplace.small_runs();
   std::vector<DmaRun> runs;
 
   auto unpack = [&](Staging::Slot &sl) -> int {
@@ -1009,7 +1071,32 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
       const size_t in_bytes = static_cast<size_t>(nb) * nin * len;
       const size_t out_off = in_bytes;
       hipError_t err;
-      if (pinned) {
+      size_t npin = 0;  // kernel transport: input pieces at sl.pl[0, npin), output pieces after
+      if (by_kernel) {
+        const size_t per = (len + lsec::kPieceBytes - 1) / lsec::kPieceBytes;
+        const size_t need = per * static_cast<size_t>(nb) * (nin + nout);
+        if (sl.pl_cap < need) {
+          if (sl.pl) (void)hipHostFree(sl.pl);
+          sl.pl = nullptr;
+          sl.pl_cap = 0;
+          const size_t cap = std::max(need, per * static_cast<size_t>(nb_max) * (nin + nout));
+          if (hipHostMalloc(reinterpret_cast<void **>(&sl.pl), cap * sizeof(lsec::CopyPiece), hipHostMallocDefault) !=
+              hipSuccess) {
+            (void)hipGetLastError();
+            sl.pl = nullptr;
+            rc = fail("cannot allocate the copy-piece list");
+            break;
+          }
+          sl.pl_cap = cap;
+        }
+        for (int s = 0; s < nb; ++s)
+          for (int j = 0; j < nin; ++j)
+            if (rc == 0 && !(npin = add_pieces(sl.pl, npin, inplace.alias(ptrs[static_cast<size_t>(s0 + s) * km + in_ids[j]] + c0),
+                                              reinterpret_cast<uint64_t>(sl.d) + (static_cast<size_t>(s) * nin + j) * len, len)))
+              rc = fail("kernel transport: host chunk outside the pinned regions");
+        if (rc) break;
+        err = lsec::launch_copy_pieces(sl.pl, static_cast<int>(npin), stg->s_in);
+      } else if (pinned) {
         runs.clear();
         for (int s = 0; s < nb; ++s)
           for (int j = 0; j < nin; ++j)
@@ -1047,7 +1134,16 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
         err = lsec::launch_stripe_magic(ma, stg->s_out);
         if (err != hipSuccess) { rc = fail("magic launch: %s", hipGetErrorString(err)); break; }
       }
-      if (nout > 0 && pinned) {
+      if (nout > 0 && by_kernel) {
+        size_t n = npin;
+        for (int s = 0; s < nb; ++s)
+          for (int r = 0; r < nout; ++r)
+            if (rc == 0 && !(n = add_pieces(sl.pl, n, reinterpret_cast<uint64_t>(sl.d) + out_off + (static_cast<size_t>(s) * nout + r) * len,
+                                            inplace.alias(ptrs[static_cast<size_t>(s0 + s) * km + out_ids[r]] + c0), len)))
+              rc = fail("kernel transport: host chunk outside the pinned regions");
+        if (rc) break;
+        err = lsec::launch_copy_pieces(sl.pl + npin, static_cast<int>(n - npin), stg->s_out);
+      } else if (nout > 0 && pinned) {
         runs.clear();
         for (int s = 0; s < nb; ++s)
           for (int r = 0; r < nout; ++r)

@@ -107,6 +107,18 @@ struct GatherPiece {
 };
 hipError_t launch_gather(const GatherPiece *list, int n, char *dst, hipStream_t stream);
 
+// Host-memory transport by kernel: piece i copies bytes[i] (a multiple of 16, <= kPieceBytes)
+// from src to dst, both 16-byte aligned, one block per piece.  Either side may be the device
+// alias of page-locked host memory, so one launch moves many small host runs over PCIe
+// without a DMA command per run.  `list` must be device-readable (page-locked host is).
+constexpr uint32_t kPieceBytes = 16384;
+struct CopyPiece {
+  uint64_t src;
+  uint64_t dst;
+  uint64_t bytes;
+};
+hipError_t launch_copy_pieces(const CopyPiece *list, int n, hipStream_t stream);
+
 // HBM probe (measurement only): dst <- src, bytes a multiple of 16, both 16-byte aligned.
 hipError_t launch_hbm_copy(void *dst, const void *src, uint64_t bytes, hipStream_t stream);
 

@@ -256,7 +256,37 @@ __global__ __launch_bounds__(kBlock) void k_hbm_copy(uint64_t dst, uint64_t src,
   }
 }
 
+// A small grid striding over the pieces, every lane holding its 4 x 16 B of a piece in flight
+// before storing: enough bytes in flight for PCIe, while the H2D and D2H launches (on two
+// streams) and the coding kernel between them all keep room on the CUs.  (One block per piece
+// let each transfer fill the chip, so the two directions ran one after the other.)
+constexpr int kCopyGrid = 256;
+static_assert(kPieceBytes == kBlock * 16 * 4, "one piece = 4 x 16 B per lane");
+__global__ __launch_bounds__(kBlock) void k_copy_pieces(const CopyPiece *list, int n) {
+  for (int p = blockIdx.x; p < n; p += gridDim.x) {
+    const CopyPiece g = list[p];
+    const uint64_t n16 = g.bytes / 16;
+    u32x4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t e = threadIdx.x + static_cast<uint64_t>(i) * kBlock;
+      if (e < n16) v[i] = __builtin_nontemporal_load(gptr<u32x4>(g.src + e * 16));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t e = threadIdx.x + static_cast<uint64_t>(i) * kBlock;
+      if (e < n16) __builtin_nontemporal_store(v[i], gptr_w<u32x4>(g.dst + e * 16));
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_copy_pieces(const CopyPiece *list, int n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_copy_pieces, dim3(std::min(n, kCopyGrid)), dim3(kBlock), 0, st, list, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_hbm_copy(void *dst, const void *src, uint64_t bytes, hipStream_t st) {
   if (!dst || !src || bytes % 16 != 0 || (reinterpret_cast<uint64_t>(dst) | reinterpret_cast<uint64_t>(src)) % 16)

@@ -778,3 +778,39 @@ def test_zero_ones_and_single_bit_patterns(cuda, method, k, m, size):
             p.decode_dev(d, par, pat, out=out)
             torch.cuda.synchronize()
             assert np.array_equal(out.cpu().numpy(), full[:, pat]), pat
+
+
+@pytest.mark.parametrize("method,k,m,size,n,shift", [(L.REED_SOL_VAN, 6, 3, 64 << 10, 200, 0),
+                                                     (L.CAUCHY_GOOD, 10, 4, 256 << 10, 16, 0),
+                                                     (L.REED_SOL_VAN, 20, 6, 32 << 10, 120, 0),
+                                                     (L.REED_SOL_VAN, 6, 3, 64 << 10, 200, 8)])
+def test_pageable_small_runs_by_kernel(cuda, method, k, m, size, n, shift):
+    """With LSEC_KERNEL_COPY=1, large pageable batches of small chunks (LStore's [stripe][k+m][C]
+    pages, runs well under 4 MiB) are pinned in place and moved by the copy-piece kernel over
+    their device aliases;
+    8-byte-misaligned buffers (shift=8) cannot be, and pack.  Encode and a double-erasure
+    decode are bit-exact either way."""
+    import os
+
+    os.environ["LSEC_KERNEL_COPY"] = "1"   # opt-in transport, read per call
+    try:
+        _small_runs_case(method, k, m, size, n, shift)
+    finally:
+        del os.environ["LSEC_KERNEL_COPY"]
+
+
+def _small_runs_case(method, k, m, size, n, shift):
+    raw = np.zeros(n * (k + m) * size + 64, dtype=np.uint8)
+    off = (-raw.ctypes.data) % 16 + shift
+    st = raw[off:off + n * (k + m) * size].reshape(n, k + m, size)
+    st[:, :k] = np.random.default_rng(size + k).integers(0, 256, (n, k, size), dtype=np.uint8)
+    with L.Plan.for_chunk(method, k, m, size) as p:
+        p.encode_stripes(st)
+        for s in (0, n // 3, n - 1):
+            assert np.array_equal(st[s, k:], O.encode(method, st[s, :k], m, p.packet_size)), s
+        full = st.copy()
+        p.encode_stripes(st)                         # repeat: slots and piece lists reused
+        assert np.array_equal(st, full)
+        st[:, [1, k + m - 1]] = 0xA5
+        p.decode_stripes(st, [1, k + m - 1])
+        assert np.array_equal(st, full)

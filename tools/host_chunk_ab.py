@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Host-path rate vs chunk size (development probe): et_encode_stripes / et_decode_stripes over
 ~1 GiB of user data in one (N, k+m, C) host array, median of --reps calls, for pageable and
-page-locked callers.  Run once per LSEC_NO_HOST_REGISTER setting (tools/gpu_host_chunk_ab.sh)."""
+page-locked callers.  Run once per LSEC_NO_HOST_REGISTER / LSEC_KERNEL_COPY setting
+(tools/gpu_host_chunk_ab.sh, tools/gpu_kcopy_ab.sh; kcopy = small runs moved by kernel)."""
 import argparse
 import os
 import sys
@@ -25,7 +26,8 @@ def main():
 
     import lstore_amd as L
 
-    mode = "packed" if os.environ.get("LSEC_NO_HOST_REGISTER") else "inplace"
+    mode = ("packed" if os.environ.get("LSEC_NO_HOST_REGISTER") else
+            "kcopy" if os.environ.get("LSEC_KERNEL_COPY") == "1" else "inplace")
     k, m = a.k, a.m
     for C in [int(x) for x in a.chunks.split(",")]:
         n = max(2, int(a.gib * 2**30 / (k * C)))
