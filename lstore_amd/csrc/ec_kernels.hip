@@ -284,7 +284,11 @@ __global__ __launch_bounds__(kBlock) void k_copy_pieces(const CopyPiece *list, i
 
 hipError_t launch_copy_pieces(const CopyPiece *list, int n, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_copy_pieces, dim3(std::min(n, kCopyGrid)), dim3(kBlock), 0, st, list, n);
+  static const int grid_cap = [] {  // LSEC_COPY_GRID: A/B runs of the transport's footprint
+    const char *s = getenv("LSEC_COPY_GRID");
+    return s ? std::max(1, atoi(s)) : kCopyGrid;
+  }();
+  hipLaunchKernelGGL(k_copy_pieces, dim3(std::min(n, grid_cap)), dim3(kBlock), 0, st, list, n);
   return hipGetLastError();
 }
 
