@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdint>
@@ -1033,6 +1034,13 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   // pinned callers (or pageable ones pinned in place for this call): DMA straight between
   // their buffers and the device slots.  `inplace` is declared before the staging users, so
   // its registrations outlive every DMA (all are drained before run_host returns).
+  // LSEC_TRACE=1: wall time of the phases of this call on stderr
+  static const bool trace = getenv("LSEC_TRACE") != nullptr;
+  const auto now = [] { return std::chrono::steady_clock::now(); };
+  const auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  };
+  const auto t_pin0 = now();
   InPlacePin inplace;
   const bool kernel_ok = kernel_transport_ok(ptrs, nstripes, km, in_ids, out_ids, C, cb);
   const bool pinned = pinned_layout(ptrs, nstripes, km, in_ids, out_ids) ||
@@ -1041,6 +1049,7 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   // direction instead of a DMA per run (each DMA from registered pageable memory costs ~50 us;
   // 256 KiB runs move at 18 GB/s by DMA, 54 GB/s by one kernel: profiles/r01_v27_zerocopy_probe.txt)
   const bool by_kernel = inplace.small_runs();
+  const auto t_loop0 = now();
   std::vector<DmaRun> runs;
 
   auto unpack = [&](Staging::Slot &sl) -> int {
@@ -1169,10 +1178,20 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
     if (err == hipSuccess) err = hipMemcpyAsync(magic_host, dmagic, 4ull * nstripes, hipMemcpyDeviceToHost, stg->s_out);
     if (err != hipSuccess) rc = fail("magic finalize: %s", hipGetErrorString(err));
   }
+  const auto t_drain0 = now();
   // drain in submission order
   for (int i = 0; i < kSlots; ++i) {
     const int r2 = unpack(stg->slot[(which + i) % kSlots]);
     if (!rc) rc = r2;
+  }
+  if (trace && rc == 0) {  // every slot drained: no transfer still reads or writes the pins
+    const auto t_rel0 = now();
+    inplace.release();  // (the destructor would, after this print)
+    const auto t_end = now();
+    fprintf(stderr, "[lsec trace] host call %d stripes, %d in / %d out x %lld B (%s): pin %.2f ms, submit %.2f ms, "
+                    "drain %.2f ms, unpin %.2f ms\n",
+            nstripes, nin, nout, C, by_kernel ? "kernel transport" : pinned ? "pinned DMA" : "packed", ms(t_pin0, t_loop0),
+            ms(t_loop0, t_drain0), ms(t_drain0, t_rel0), ms(t_rel0, t_end));
   }
   if (dacc) {
     if (hipStreamSynchronize(stg->s_out) != hipSuccess && !rc) rc = fail("magic sync failed");
