@@ -1049,6 +1049,10 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   // direction instead of a DMA per run (each DMA from registered pageable memory costs ~50 us;
   // 256 KiB runs move at 18 GB/s by DMA, 54 GB/s by one kernel: profiles/r01_v27_zerocopy_probe.txt)
   const bool by_kernel = inplace.small_runs();
+  // Outputs go back by kernel too.  GPU-initiated reads and writes of host memory share ~52 GB/s
+  // (profiles/r01_v28_host_trace.txt), but DMA of the same small registered runs is slower still:
+  // kernel in + DMA out gave 17-30 GiB/s encode against 28-32 (profiles/r01_v28_kcopy_modes.txt).
+  const bool out_by_kernel = by_kernel;
   const auto t_loop0 = now();
   std::vector<DmaRun> runs;
 
@@ -1143,7 +1147,7 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
         err = lsec::launch_stripe_magic(ma, stg->s_out);
         if (err != hipSuccess) { rc = fail("magic launch: %s", hipGetErrorString(err)); break; }
       }
-      if (nout > 0 && by_kernel) {
+      if (nout > 0 && out_by_kernel) {
         size_t n = npin;
         for (int s = 0; s < nb; ++s)
           for (int r = 0; r < nout; ++r)
