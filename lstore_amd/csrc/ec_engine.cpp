@@ -1031,9 +1031,6 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
     dmagic = reinterpret_cast<uint8_t *>(dacc + 2ull * nstripes);
   }
 
-  // pinned callers (or pageable ones pinned in place for this call): DMA straight between
-  // their buffers and the device slots.  `inplace` is declared before the staging users, so
-  // its registrations outlive every DMA (all are drained before run_host returns).
   // LSEC_TRACE=1: wall time of the phases of this call on stderr
   static const bool trace = getenv("LSEC_TRACE") != nullptr;
   const auto now = [] { return std::chrono::steady_clock::now(); };
@@ -1041,6 +1038,9 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
     return std::chrono::duration<double, std::milli>(b - a).count();
   };
   const auto t_pin0 = now();
+  // pinned callers (or pageable ones pinned in place for this call): DMA straight between
+  // their buffers and the device slots.  `inplace` is declared before the staging users, so
+  // its registrations outlive every DMA (all are drained before run_host returns).
   InPlacePin inplace;
   const bool kernel_ok = kernel_transport_ok(ptrs, nstripes, km, in_ids, out_ids, C, cb);
   const bool pinned = pinned_layout(ptrs, nstripes, km, in_ids, out_ids) ||
