@@ -955,19 +955,78 @@ size_t add_pieces(lsec::CopyPiece *pl, size_t n, uint64_t src, uint64_t dst, siz
   return n;
 }
 
-// Opt-in (LSEC_KERNEL_COPY=1, read per call): large pageable batches of small host runs are
-// pinned in place and moved by kernel over their device aliases instead of being packed.
-// Needs every transferred chunk (and column block) 16-byte aligned.  Not the default: on the
-// box it held 29-32 GiB/s encode / 36-41 decode for C = 64-512 KiB whatever the host cores
-// did, while packing ran 23-38 / 28-45 depending on them (profiles/r01_v27_kernel_copy_ab.txt).
-bool kernel_transport_ok(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids,
-                         const std::vector<int> &out_ids, long long C, long long cb) {
+// Kernel transport policy, LSEC_KERNEL_COPY read per call:
+//   unset  caller page-locked buffers with small runs move by kernel (DMA of their 384 KiB runs
+//          moves 17-20 GiB/s at C = 64 KiB, the kernel 30 / 38: profiles/r01_v28_kcopy_pinned.txt);
+//          pageable batches with small runs are packed
+//   1      pageable ones too: pinned in place and moved by kernel over their device aliases (it
+//          held 29-32 GiB/s encode / 36-41 decode for C = 64-512 KiB whatever the host cores did,
+//          where packing ran 23-38 / 28-45 depending on them: r01_v27_kernel_copy_ab.txt)
+//   0      never
+enum class KernelCopy { kNever, kCallerPinned, kAll };
+KernelCopy kernel_copy_policy() {
   const char *on = getenv("LSEC_KERNEL_COPY");
-  if (!on || *on != '1' || C % 16 != 0 || cb % 16 != 0) return false;
+  if (!on || !*on) return KernelCopy::kCallerPinned;
+  return *on == '1' ? KernelCopy::kAll : *on == '0' ? KernelCopy::kNever : KernelCopy::kCallerPinned;
+}
+
+// every transferred chunk (and column block) 16-byte aligned, as the copy-piece kernel needs
+bool kernel_transport_aligned(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids,
+                              const std::vector<int> &out_ids, long long C, long long cb) {
+  if (C % 16 != 0 || cb % 16 != 0) return false;
   for (int s = 0; s < nstripes; ++s)
     for (const std::vector<int> *ids : {&in_ids, &out_ids})
       for (int id : *ids)
         if (reinterpret_cast<uintptr_t>(ptrs[static_cast<size_t>(s) * km + id]) % 16 != 0) return false;
+  return true;
+}
+
+// Caller page-locked buffers with small runs (average < 1 MiB: DMA of 384 KiB runs from
+// hipHostMalloc memory moves ~20 GiB/s, profiles/r01_v27_kernel_copy_ab.txt) move by kernel,
+// once EVERY chunk is checked: page-locked, inside one allocation, with a device address
+// (a pageable chunk between pinned ones is harmless to a DMA but would fault a kernel).  The
+// check costs ~0.06 us per chunk (tools/probes/pinned_attr_probe.cpp).  dev[i] gets the device
+// address of chunk i, in the order stripe, then in_ids, then out_ids.
+bool caller_pinned_aliases(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids,
+                           const std::vector<int> &out_ids, long long C, std::vector<uint64_t> &dev) {
+  size_t runs = 0, total = 0;
+  for (const std::vector<int> *ids : {&in_ids, &out_ids}) {
+    const char *end = nullptr;
+    for (int s = 0; s < nstripes; ++s)
+      for (int id : *ids) {
+        const char *b = ptrs[static_cast<size_t>(s) * km + id];
+        if (b != end) ++runs;
+        end = b + C;
+        total += static_cast<size_t>(C);
+      }
+  }
+  if (runs == 0 || total / runs >= (1ull << 20)) return false;
+  dev.clear();
+  dev.reserve(static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()));
+  uintptr_t lo = 1, hi = 0;  // last allocation seen [lo, hi)
+  for (int s = 0; s < nstripes; ++s)
+    for (const std::vector<int> *ids : {&in_ids, &out_ids})
+      for (int id : *ids) {
+        char *p = ptrs[static_cast<size_t>(s) * km + id];
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer) {
+          (void)hipGetLastError();
+          return false;
+        }
+        const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+        if (u < lo || u + static_cast<uintptr_t>(C) > hi) {
+          hipDeviceptr_t base = nullptr;
+          size_t size = 0;
+          if (hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(p)) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+          }
+          lo = reinterpret_cast<uintptr_t>(base);
+          hi = lo + size;
+          if (u < lo || u + static_cast<uintptr_t>(C) > hi) return false;
+        }
+        dev.push_back(reinterpret_cast<uint64_t>(a.devicePointer));
+      }
   return true;
 }
 
@@ -1042,13 +1101,24 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   // their buffers and the device slots.  `inplace` is declared before the staging users, so
   // its registrations outlive every DMA (all are drained before run_host returns).
   InPlacePin inplace;
-  const bool kernel_ok = kernel_transport_ok(ptrs, nstripes, km, in_ids, out_ids, C, cb);
-  const bool pinned = pinned_layout(ptrs, nstripes, km, in_ids, out_ids) ||
-                      inplace.pin(ptrs, nstripes, km, in_ids, out_ids, C, kernel_ok);
+  const KernelCopy kpol = kernel_copy_policy();
+  const bool aligned = kpol != KernelCopy::kNever && kernel_transport_aligned(ptrs, nstripes, km, in_ids, out_ids, C, cb);
+  const bool caller_pinned = pinned_layout(ptrs, nstripes, km, in_ids, out_ids);
+  const bool pinned =
+      caller_pinned || inplace.pin(ptrs, nstripes, km, in_ids, out_ids, C, aligned && kpol == KernelCopy::kAll);
+  std::vector<uint64_t> calias;  // caller-pinned chunks moved by kernel: their device addresses
+  const bool caller_by_kernel =
+      caller_pinned && aligned && caller_pinned_aliases(ptrs, nstripes, km, in_ids, out_ids, C, calias);
+  const size_t nio = in_ids.size() + out_ids.size();
+  // device address of byte c0 of chunk (stripe s, list position i: inputs, then outputs)
+  const auto dev_at = [&](int s, size_t i, int id, long long c0) -> uint64_t {
+    if (caller_by_kernel) return calias[static_cast<size_t>(s) * nio + i] + static_cast<uint64_t>(c0);
+    return inplace.alias(ptrs[static_cast<size_t>(s) * km + id] + c0);
+  };
   // small host runs pinned in place move by kernel over their device aliases: one launch per
   // direction instead of a DMA per run (each DMA from registered pageable memory costs ~50 us;
   // 256 KiB runs move at 18 GB/s by DMA, 54 GB/s by one kernel: profiles/r01_v27_zerocopy_probe.txt)
-  const bool by_kernel = inplace.small_runs();
+  const bool by_kernel = inplace.small_runs() || caller_by_kernel;
   // Outputs go back by kernel too.  GPU-initiated reads and writes of host memory share ~52 GB/s
   // (profiles/r01_v28_host_trace.txt), but DMA of the same small registered runs is slower still:
   // kernel in + DMA out gave 17-30 GiB/s encode against 28-32 (profiles/r01_v28_kcopy_modes.txt).
@@ -1104,7 +1174,7 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
         }
         for (int s = 0; s < nb; ++s)
           for (int j = 0; j < nin; ++j)
-            if (rc == 0 && !(npin = add_pieces(sl.pl, npin, inplace.alias(ptrs[static_cast<size_t>(s0 + s) * km + in_ids[j]] + c0),
+            if (rc == 0 && !(npin = add_pieces(sl.pl, npin, dev_at(s0 + s, static_cast<size_t>(j), in_ids[j], c0),
                                               reinterpret_cast<uint64_t>(sl.d) + (static_cast<size_t>(s) * nin + j) * len, len)))
               rc = fail("kernel transport: host chunk outside the pinned regions");
         if (rc) break;
@@ -1152,7 +1222,7 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
         for (int s = 0; s < nb; ++s)
           for (int r = 0; r < nout; ++r)
             if (rc == 0 && !(n = add_pieces(sl.pl, n, reinterpret_cast<uint64_t>(sl.d) + out_off + (static_cast<size_t>(s) * nout + r) * len,
-                                            inplace.alias(ptrs[static_cast<size_t>(s0 + s) * km + out_ids[r]] + c0), len)))
+                                            dev_at(s0 + s, static_cast<size_t>(nin + r), out_ids[r], c0), len)))
               rc = fail("kernel transport: host chunk outside the pinned regions");
         if (rc) break;
         err = lsec::launch_copy_pieces(sl.pl + npin, static_cast<int>(n - npin), stg->s_out);

@@ -780,27 +780,38 @@ def test_zero_ones_and_single_bit_patterns(cuda, method, k, m, size):
             assert np.array_equal(out.cpu().numpy(), full[:, pat]), pat
 
 
-@pytest.mark.parametrize("method,k,m,size,n,shift", [(L.REED_SOL_VAN, 6, 3, 64 << 10, 200, 0),
-                                                     (L.CAUCHY_GOOD, 10, 4, 256 << 10, 16, 0),
-                                                     (L.REED_SOL_VAN, 20, 6, 32 << 10, 120, 0),
-                                                     (L.REED_SOL_VAN, 6, 3, 64 << 10, 200, 8)])
-def test_pageable_small_runs_by_kernel(cuda, method, k, m, size, n, shift):
+@pytest.mark.parametrize("method,k,m,size,n,shift,pinned", [(L.REED_SOL_VAN, 6, 3, 64 << 10, 200, 0, False),
+                                                            (L.CAUCHY_GOOD, 10, 4, 256 << 10, 16, 0, False),
+                                                            (L.REED_SOL_VAN, 20, 6, 32 << 10, 120, 0, False),
+                                                            (L.REED_SOL_VAN, 6, 3, 64 << 10, 200, 8, False),
+                                                            (L.REED_SOL_VAN, 6, 3, 64 << 10, 200, 0, True),
+                                                            (L.CAUCHY_GOOD, 6, 3, 64 << 10, 64, 0, True),
+                                                            (L.REED_SOL_VAN, 6, 3, 64 << 10, 40, 8, True)])
+def test_pageable_small_runs_by_kernel(cuda, method, k, m, size, n, shift, pinned):
     """With LSEC_KERNEL_COPY=1, large pageable batches of small chunks (LStore's [stripe][k+m][C]
     pages, runs well under 4 MiB) are pinned in place and moved by the copy-piece kernel over
-    their device aliases;
-    8-byte-misaligned buffers (shift=8) cannot be, and pack.  Encode and a double-erasure
-    decode are bit-exact either way."""
+    their device aliases (by default they pack);
+    8-byte-misaligned buffers (shift=8) cannot be, and pack.  Caller page-locked buffers
+    (pinned=True) with small runs move by kernel by default, after every chunk is checked;
+    misaligned ones DMA.  Encode and a double-erasure decode are bit-exact either way."""
     import os
 
-    os.environ["LSEC_KERNEL_COPY"] = "1"   # opt-in transport, read per call
+    if pinned:                              # caller page-locked: kernel transport by default
+        _small_runs_case(method, k, m, size, n, shift, pinned)
+        return
+    os.environ["LSEC_KERNEL_COPY"] = "1"    # pageable: opt-in, read per call
     try:
-        _small_runs_case(method, k, m, size, n, shift)
+        _small_runs_case(method, k, m, size, n, shift, pinned)
     finally:
         del os.environ["LSEC_KERNEL_COPY"]
 
 
-def _small_runs_case(method, k, m, size, n, shift):
-    raw = np.zeros(n * (k + m) * size + 64, dtype=np.uint8)
+def _small_runs_case(method, k, m, size, n, shift, pinned):
+    if pinned:
+        import torch
+        raw = torch.zeros(n * (k + m) * size + 64, dtype=torch.uint8, pin_memory=True).numpy()
+    else:
+        raw = np.zeros(n * (k + m) * size + 64, dtype=np.uint8)
     off = (-raw.ctypes.data) % 16 + shift
     st = raw[off:off + n * (k + m) * size].reshape(n, k + m, size)
     st[:, :k] = np.random.default_rng(size + k).integers(0, 256, (n, k, size), dtype=np.uint8)
