@@ -1030,6 +1030,10 @@ bool caller_pinned_aliases(char **ptrs, int nstripes, int km, const std::vector<
   return true;
 }
 
+void split_pieces(std::vector<lsec::CopyPiece> &v, uint64_t src, uint64_t dst, size_t len) {
+  for (size_t o = 0; o < len; o += lsec::kPieceBytes) v.push_back({src + o, dst + o, std::min<uint64_t>(lsec::kPieceBytes, len - o)});
+}
+
 hipError_t issue_runs(const std::vector<DmaRun> &v, hipMemcpyKind kind, hipStream_t st) {
   for (const DmaRun &r : v) {
     const hipError_t e = hipMemcpyAsync(r.dst, r.src, r.bytes, kind, st);
@@ -1332,6 +1336,10 @@ struct HostReq {
   char **ptrs = nullptr;
   int nstripes = 0, km = 0, kind = 0, packet = 0, w = 8;
   bool pinned = false;  // caller buffers page-locked: DMA in place, no packing
+  // pinned with small runs, every chunk checked: moved by the copy-piece kernel; dev = the
+  // chunks' device addresses (stripe, then in_ids, then out_ids -- caller_pinned_aliases)
+  bool by_kernel = false;
+  std::vector<uint64_t> dev;
   long long C = 0;
   std::vector<int> in_ids, out_ids;
   const void *image = nullptr;
@@ -1390,6 +1398,8 @@ class Dispatcher {
   struct Slot {
     char *d = nullptr, *h = nullptr;
     size_t cap = 0;
+    lsec::CopyPiece *pl = nullptr;  // copy pieces of by_kernel requests (page-locked)
+    size_t pl_cap = 0;
     hipEvent_t done = nullptr;
     std::vector<Group> groups;
     std::string err;
@@ -1408,6 +1418,10 @@ class Dispatcher {
     if (sl.groups.empty()) return;
     std::string err = sl.err;
     if (err.empty() && hipEventSynchronize(sl.done) != hipSuccess) err = "dispatcher: event sync failed";
+    if (!err.empty()) {  // whatever was enqueued must not outlive the callers' buffers or the slot
+      (void)hipStreamSynchronize(s_in_);
+      (void)hipStreamSynchronize(s_out_);
+    }
     std::vector<CopyJob> jobs;
     if (err.empty()) {
       for (const Group &g : sl.groups) {
@@ -1478,6 +1492,7 @@ class Dispatcher {
     // mirror that (finish() unpacks only the pageable ones).
     std::vector<CopyJob> jobs;
     std::vector<DmaRun> h2d, d2h;
+    std::vector<lsec::CopyPiece> kin, kout;  // by_kernel requests
     for (const Group &g : sl.groups) {
       const HostReq &r0 = *g.reqs[0];
       const size_t C = static_cast<size_t>(r0.C), nin = r0.in_ids.size(), nout = r0.out_ids.size();
@@ -1486,7 +1501,16 @@ class Dispatcher {
         const HostReq &r = *g.reqs[q];
         const size_t ib = g.off + static_cast<size_t>(g.first[q]) * nin * C;
         const size_t ob = out0 + static_cast<size_t>(g.first[q]) * nout * C;
-        if (r.pinned) {
+        if (r.by_kernel) {
+          const size_t nio = nin + nout;
+          for (int s = 0; s < r.nstripes; ++s) {
+            for (size_t j = 0; j < nin; ++j)
+              split_pieces(kin, r.dev[s * nio + j], reinterpret_cast<uint64_t>(sl.d) + ib + (static_cast<size_t>(s) * nin + j) * C, C);
+            for (size_t o = 0; o < nout; ++o)
+              split_pieces(kout, reinterpret_cast<uint64_t>(sl.d) + ob + (static_cast<size_t>(s) * nout + o) * C,
+                           r.dev[s * nio + nin + o], C);
+          }
+        } else if (r.pinned) {
           for (int s = 0; s < r.nstripes; ++s) {
             for (size_t j = 0; j < nin; ++j)
               add_run(h2d, sl.d + ib + (static_cast<size_t>(s) * nin + j) * C, r.ptrs[static_cast<size_t>(s) * r.km + r.in_ids[j]], C);
@@ -1503,7 +1527,25 @@ class Dispatcher {
       }
     }
     CopyPool::get().run(jobs);
+    if (!kin.empty() || !kout.empty()) {
+      const size_t need = kin.size() + kout.size();
+      if (sl.pl_cap < need) {
+        const size_t cap = std::max(need, 2 * sl.pl_cap + 4096);
+        if (sl.pl) (void)hipHostFree(sl.pl);
+        sl.pl = nullptr;
+        sl.pl_cap = 0;
+        if (!hip_err(hipHostMalloc(reinterpret_cast<void **>(&sl.pl), cap * sizeof(lsec::CopyPiece), hipHostMallocDefault),
+                     "hipHostMalloc")) {
+          sl.pl = nullptr;
+          return;
+        }
+        sl.pl_cap = cap;
+      }
+      std::copy(kin.begin(), kin.end(), sl.pl);
+      std::copy(kout.begin(), kout.end(), sl.pl + kin.size());
+    }
     if (!hip_err(issue_runs(h2d, hipMemcpyHostToDevice, s_in_), "H2D")) return;
+    if (!kin.empty() && !hip_err(lsec::launch_copy_pieces(sl.pl, static_cast<int>(kin.size()), s_in_), "H2D pieces")) return;
     if (!hip_err(hipEventRecord(in_done_, s_in_), "event") || !hip_err(hipStreamWaitEvent(s_out_, in_done_, 0), "wait"))
       return;
     for (const Group &g : sl.groups) {
@@ -1523,6 +1565,9 @@ class Dispatcher {
       }
     }
     if (!hip_err(issue_runs(d2h, hipMemcpyDeviceToHost, s_out_), "D2H")) return;
+    if (!kout.empty() &&
+        !hip_err(lsec::launch_copy_pieces(sl.pl + kin.size(), static_cast<int>(kout.size()), s_out_), "D2H pieces"))
+      return;
     hip_err(hipEventRecord(sl.done, s_out_), "event");
   }
 
@@ -1593,6 +1638,9 @@ int run_coalesced(PlanExt *e, char **ptrs, int nstripes, long long C, const std:
   r.packet = e->pub.packet_size;
   r.w = e->pub.w;
   r.pinned = pinned_layout(ptrs, nstripes, r.km, in_ids, out_ids);
+  r.by_kernel = r.pinned && kernel_copy_policy() != KernelCopy::kNever &&
+                kernel_transport_aligned(ptrs, nstripes, r.km, in_ids, out_ids, C, C) &&
+                caller_pinned_aliases(ptrs, nstripes, r.km, in_ids, out_ids, C, r.dev);
   return Dispatcher::for_device(dev)->run(r);
 }
 

@@ -539,13 +539,15 @@ def test_pageable_batches_pinned_in_place_share_inputs(cuda):
         assert np.array_equal(st, full)
 
 
-def test_fn_pointer_pinned_and_pageable_callers_coalesced(cuda):
+@pytest.mark.parametrize("method", [L.REED_SOL_VAN, L.CAUCHY_GOOD])
+def test_fn_pointer_pinned_and_pageable_callers_coalesced(cuda, method):
     """Concurrent single-stripe calls, half on page-locked and half on pageable buffers, go
-    through the dispatcher together; each gets its own parity and rebuilds."""
+    through the dispatcher together; each gets its own parity and rebuilds.  The page-locked
+    ones (384 KiB runs) move by the copy-piece kernel, the pageable ones are packed."""
     import threading
 
     k, m, size = 6, 3, 65536
-    with L.Plan.for_chunk(L.REED_SOL_VAN, k, m, size) as p:
+    with L.Plan.for_chunk(method, k, m, size) as p:
         errors = []
 
         def worker(t):
@@ -556,7 +558,7 @@ def test_fn_pointer_pinned_and_pageable_callers_coalesced(cuda):
                     sh[:k] = rng.integers(0, 256, (k, size), dtype=np.uint8)
                     sh[k:] = 0
                     p.encode_block([sh[i] for i in range(k + m)])
-                    if not np.array_equal(sh[k:], O.encode(O.REED_SOL_VAN, sh[:k], m)):
+                    if not np.array_equal(sh[k:], O.encode(method, sh[:k], m, p.packet_size)):
                         errors.append((t, it, "encode"))
                     full = sh.copy()
                     lost = [(t + it) % (k + m)]

@@ -10,7 +10,10 @@
  * build: gcc -O2 -o build/fnptr_bench tools/fnptr_bench.c -Iinclude -Llstore_amd -llstore_ec \
  *            -Wl,-rpath,'$ORIGIN/../lstore_amd' -lpthread
  * run:   build/fnptr_bench <chunk> <threads> <calls_per_thread> [method]
+ *        FNPTR_PINNED=1: each thread's buffer is page-locked (hipHostMalloc, looked up at run
+ *        time from libamdhip64.so), as an LStore cache that pins its pages would hold it
  */
+#include <dlfcn.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -20,6 +23,8 @@
 #include "lstore_ec.h"
 
 static lio_erasure_plan_t *g_plan;
+static int (*g_host_malloc)(void **, size_t, unsigned);
+static int (*g_host_free)(void *);
 static int g_chunk, g_calls;
 static double *g_lat;
 
@@ -34,7 +39,13 @@ static void *worker(void *arg)
 {
     long t = (long)arg;
     int k = g_plan->data_strips, m = g_plan->parity_strips;
-    char *buf = malloc((size_t)(k + m) * g_chunk);
+    char *buf = NULL;
+    if (g_host_malloc) {
+        if (g_host_malloc((void **)&buf, (size_t)(k + m) * g_chunk, 0) != 0) buf = NULL;
+    } else {
+        buf = malloc((size_t)(k + m) * g_chunk);
+    }
+    if (!buf) return NULL;
     char *ptr[64];
     for (size_t i = 0; i < (size_t)(k + m) * g_chunk; i++) buf[i] = (char)(i * 131 + t);
     for (int i = 0; i < k + m; i++) ptr[i] = buf + (size_t)i * g_chunk;
@@ -43,7 +54,8 @@ static void *worker(void *arg)
         g_plan->encode_block(g_plan, ptr, g_chunk);     /* segment/jerasure.c:1847 */
         g_lat[t * g_calls + c] = now() - t0;
     }
-    free(buf);
+    if (g_host_malloc) g_host_free(buf);
+    else free(buf);
     return NULL;
 }
 
@@ -55,6 +67,17 @@ static int cmp(const void *a, const void *b)
 
 int main(int argc, char **argv)
 {
+    if (getenv("FNPTR_PINNED") && atoi(getenv("FNPTR_PINNED"))) {
+        void *h = dlopen("libamdhip64.so", RTLD_NOW | RTLD_GLOBAL);
+        if (h) {
+            g_host_malloc = (int (*)(void **, size_t, unsigned))dlsym(h, "hipHostMalloc");
+            g_host_free = (int (*)(void *))dlsym(h, "hipHostFree");
+        }
+        if (!g_host_malloc || !g_host_free) {
+            fprintf(stderr, "FNPTR_PINNED: hipHostMalloc not found\n");
+            return 1;
+        }
+    }
     g_chunk = argc > 1 ? atoi(argv[1]) : 16384;
     int T = argc > 2 ? atoi(argv[2]) : 8;
     g_calls = argc > 3 ? atoi(argv[3]) : 200;
@@ -79,8 +102,10 @@ int main(int argc, char **argv)
     double wall = now() - t0;
     size_t n = (size_t)T * g_calls;
     qsort(g_lat, n, sizeof(double), cmp);
-    printf("{\"chunk\": %d, \"threads\": %d, \"calls\": %zu, \"method\": \"%s\", \"per_call_us_p50\": %.1f, "
-           "\"per_call_us_p99\": %.1f, \"gibps\": %.3f}\n", g_chunk, T, n, JE_method[method],
+    const char *kc = getenv("LSEC_KERNEL_COPY");
+    printf("{\"chunk\": %d, \"threads\": %d, \"calls\": %zu, \"method\": \"%s\", \"pinned\": %d, \"kernel_copy\": \"%s\", "
+           "\"per_call_us_p50\": %.1f, \"per_call_us_p99\": %.1f, \"gibps\": %.3f}\n", g_chunk, T, n, JE_method[method],
+           g_host_malloc != NULL, kc ? kc : "default",
            g_lat[n / 2] * 1e6, g_lat[(size_t)(n * 0.99)] * 1e6, n * (double)k * g_chunk / wall / (1 << 30));
     et_destroy_plan(g_plan);
     free(g_lat);
