@@ -41,10 +41,16 @@ def main():
             "max(vgpr_count + accum_vgpr_count), max(sgpr_count) from kernels group by name, grid_x "
             "order by sum(duration) desc").fetchall()
     first = next((int(a.split("=", 1)[1]) for a in sys.argv[1:] if a.startswith("--first=")), 0)
-    if first and not args[0].endswith(".csv"):
+    if first:
         per = {}
-        for name, gx, d, vg, sg in db.execute(
-                "select name, grid_x, duration, vgpr_count + accum_vgpr_count, sgpr_count from kernels order by start"):
+        if args[0].endswith(".csv"):
+            recs = sorted(csv.DictReader(open(args[0])), key=lambda r: int(r["Start_Timestamp"]))
+            launches = ((r["Kernel_Name"], int(r["Grid_Size_X"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
+                         int(r["VGPR_Count"]) + int(r["Accum_VGPR_Count"]), int(r["SGPR_Count"])) for r in recs)
+        else:
+            launches = db.execute("select name, grid_x, duration, vgpr_count + accum_vgpr_count, sgpr_count "
+                                  "from kernels order by start")
+        for name, gx, d, vg, sg in launches:
             per.setdefault((name, gx), []).append((d, vg, sg))
         rows = []
         for (name, gx), v in per.items():
