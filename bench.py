@@ -6,28 +6,37 @@ A step = encode N stripes (k data -> m parity) + decode the same N stripes with 
 lost (k survivors -> 1 rebuilt shard), both through liblstore_ec.so's device-resident C ABI
 (lsec_encode_dev / lsec_decode_dev) on the current torch stream.  Stripes are independent,
 so ranks each own N stripes (static partition, weak scaling, no collective on the data
-path; the only collectives are the timing barrier and the max-over-ranks reduction).
+path; the only collectives are the timing barrier, the max-over-ranks reduction and the
+gather of per-rank figures at the end).
 
 value = k*C*N*world / max_rank(step time) / 2^30  (data GiB/s, "N KiB stripes" = C per shard)
 
-Device-resident layout: data [N][k][C], parity [N][m][C], every shard row followed by --pad
-(default 1024) unused bytes, so the k+m streams of a stripe do not start on the same HBM
-channel (shards exactly 1 MiB apart cost the encode ~8 %: profiles/r01_v15_pad_ab.txt).
-layout.unpadded reports the same stripes with shards exactly C apart, launch-timed.
+Launching.  `bench.py --gpus N` with WORLD_SIZE unset starts N ranks itself (spawned before
+anything touches the GPU); under torch.distributed.run (WORLD_SIZE set) it runs as one rank
+and refuses a WORLD_SIZE that disagrees with --gpus.  LSEC_DIST_BACKEND=gloo lets the ranks
+share one GPU (rehearsal); the default is RCCL ("nccl").
+
+Device-resident layout: data [N][k][C], parity [N][m][C] -- LStore's own layout (one cache
+page holds a stripe's k chunks back to back, cache.c:3843; the parity buffer holds m,
+segment/jerasure.c:1836).  --pad B leaves B unused bytes after every shard row instead;
+layout.padded reports the same stripes with a 1 KiB pad, launch-timed, for the record.
 
 Also reported (same JSON line):
   roofline      encode kernel: algorithmic HBM bytes (k+m)*C*N per launch / avg launch time
                 (HIP events on the launch stream) vs 8 TB/s
+  per_rank      every rank's own encode / decode launch rates and roofline fractions
   cpu_baseline  the reference CPU path (oracle/_ref: vendor/jerasure via the plan dispatch)
-                on a bounded sample of the same workload, on this box's host cores
+                on a bounded sample of the same workload, at 1 thread and at every usable
+                host core of this box
   host_path     PCIe-inclusive rate of et_encode_stripes / et_decode_stripes from host memory
   hbm_copy_ref  this box's device-to-device copy rate (the practical HBM ceiling) and the
                 encode / decode kernels' rates relative to it
-Every run checks parity bit-exactly against the CPU oracle on sampled stripes.
+Every run checks parity bit-exactly against the reference (oracle/_ref) on sampled stripes.
 """
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
@@ -37,9 +46,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E (MI355X_MICROARCH.md)
+HEADLINE = "erasure encode+decode GiB/s (device-resident), RS(6+3) 1 MiB stripes"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -52,69 +62,99 @@ def parse():
     ap.add_argument("--m", type=int, default=3)
     ap.add_argument("--method", default="reed_sol_van")
     ap.add_argument("--lost", type=int, default=0, help="shard lost in the decode half")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=16.0, help="budget for the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--variant", type=str, default="0,0", help="bytewise,bitsliced kernel variants")
-    ap.add_argument("--pad", type=int, default=1024,
-                    help="bytes left unused after every shard row in HBM (0 = shards exactly C apart)")
-    ap.add_argument("--no-layout-ab", action="store_true", help="skip the unpadded-layout comparison")
+    ap.add_argument("--pad", type=int, default=0,
+                    help="bytes left unused after every shard row in HBM (0 = LStore's layout, shards exactly C apart)")
+    ap.add_argument("--no-layout-ab", action="store_true", help="skip the padded-layout comparison")
     ap.add_argument("--no-copy-ref", action="store_true", help="skip the device-copy HBM reference")
-    return ap.parse_args()
+    ap.add_argument("--json-out", default="", help="also write rank 0's JSON line to this file")
+    return ap.parse_args(argv)
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def usable_cpus():
+    """(threads to use, CPUs visible): the affinity mask, capped by the cgroup CPU quota (the
+    GPU box shows the whole machine's CPUs but grants a share of them)."""
+    visible = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(-(-int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    return (min(visible, quota) if quota else visible), visible, quota
 
 
 def cpu_baseline(method_id, k, m, C, P, lost, budget_s):
-    """Reference CPU path (oracle/_ref) on a bounded sample: encode then decode, T threads."""
+    """Reference CPU path (oracle/_ref: the real vendor/jerasure behind erasure_tools.c's
+    dispatch) on a bounded sample of the workload, called per stripe as segment/jerasure.c:1847
+    / :245 do: encode then decode(lost), at 1 thread and at every usable host core (each pthread
+    takes a contiguous stripe range)."""
+    import ctypes as Ct
+
     import oracle as O
 
     if not O.ref_available():
         return None
-    threads = max(1, min(16, os.cpu_count() or 1))
-    # about budget_s of work at ~1 GiB/s/thread encode for RS; scale by threads, cap memory
-    n = int(max(threads, min(512, budget_s * 0.5 * threads * (1 << 30) / (k * C) / 2)))
-    tile = np.random.default_rng(1).integers(0, 256, size=(min(n, 8), k + m, C), dtype=np.uint8)
-    buf = np.empty((n, k + m, C), dtype=np.uint8)
-    for s0 in range(0, n, tile.shape[0]):
-        buf[s0:s0 + tile.shape[0]] = tile[: n - s0]
-    import ctypes as Ct
-
-    base = buf.ctypes.data
-    ptrs = (Ct.c_void_p * (n * (k + m)))(*[base + i * C for i in range(n * (k + m))])
+    threads, visible, quota = usable_cpus()
     rp = O.RefPlan(method_id, k, m, 8, P)
-    rp.encode_many(ptrs, min(n, threads), C, threads)  # warm tables / pages
 
-    def passes(fn):
-        # whole passes over the n-stripe buffer (far larger than the LLC) until half the budget
-        t0, k_pass = time.perf_counter(), 0
-        while True:
-            rc = fn()
-            k_pass += 1
-            t = time.perf_counter() - t0
-            if t >= budget_s / 2:
-                return t / k_pass, k_pass, rc
+    def sample(nthreads, seconds, n):
+        tile = np.random.default_rng(1).integers(0, 256, size=(min(n, 8), k + m, C), dtype=np.uint8)
+        buf = np.empty((n, k + m, C), dtype=np.uint8)
+        for s0 in range(0, n, tile.shape[0]):
+            buf[s0:s0 + tile.shape[0]] = tile[: n - s0]
+        base = buf.ctypes.data
+        ptrs = (Ct.c_void_p * (n * (k + m)))(*[base + i * C for i in range(n * (k + m))])
+        rp.encode_many(ptrs, min(n, nthreads), C, nthreads)  # warm tables / pages
 
-    t_enc, p_enc, _ = passes(lambda: rp.encode_many(ptrs, n, C, threads))
-    t_dec, p_dec, rc = passes(lambda: rp.decode_many(ptrs, n, C, threads, [lost]))
+        def passes(fn):
+            # whole passes over the n-stripe buffer (far larger than the LLC) until the time is up
+            t0, kp = time.perf_counter(), 0
+            while True:
+                rc = fn()
+                kp += 1
+                t = time.perf_counter() - t0
+                if t >= seconds / 2:
+                    return t / kp, kp, rc
+
+        t_e, p_e, _ = passes(lambda: rp.encode_many(ptrs, n, C, nthreads))
+        t_d, p_d, rc = passes(lambda: rp.decode_many(ptrs, n, C, nthreads, [lost]))
+        gib = k * C * n / 2**30
+        return {"value": round(gib / (t_e + t_d), 3), "encode_gibps": round(gib / t_e, 3),
+                "decode_gibps": round(gib / t_d, 3), "threads": nthreads, "decode_rc": rc,
+                "sample": f"{p_e} encode + {p_d} decode(lost {lost}) passes over {n} stripes "
+                          f"({round(t_e * p_e + t_d * p_d, 1)} s)"}
+
+    stripe_bytes = (k + m) * C
+    # 1 thread: >= 512 MiB of stripes (beyond any one core's LLC slice), about 3/8 of the budget
+    one = sample(1, budget_s * 0.375, max(2, min(512, (512 << 20) // stripe_bytes + 1)))
+    allc = sample(threads, budget_s * 0.625, max(threads, min(512, (4608 << 20) // stripe_bytes + 1)))
     rp.close()
-    gib = k * C * n / 2**30
-    return {"value": round(gib / (t_enc + t_dec), 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
-            "sample": f"{p_enc} encode passes then {p_dec} decode(lost {lost}) passes over {n} stripes x {k}+{m} x {C} B "
-                      f"({round((t_enc * p_enc + t_dec * p_dec), 1)} s wall, {threads} pthreads), "
-                      f"vendor/jerasure via oracle/_ref",
-            "encode_gibps": round(gib / t_enc, 3), "decode_gibps": round(gib / t_dec, 3), "decode_rc": rc}
+    return {"value": allc["value"], "unit": "GiB/s", "cores": threads, "kind": "reference",
+            "sample": f"{allc['sample']} on {threads} pthreads; {one['sample']} on 1 thread; "
+                      f"{k}+{m} x {C} B stripes, vendor/jerasure via oracle/_ref",
+            "encode_gibps": allc["encode_gibps"], "decode_gibps": allc["decode_gibps"], "decode_rc": allc["decode_rc"],
+            "threads_1": {k2: one[k2] for k2 in ("value", "encode_gibps", "decode_gibps")},
+            "host_cpus_visible": visible, "cgroup_cpu_quota": quota}
 
 
-def pmc_traffic(k, m, C, N, kernel_kind):
-    """HBM bytes per encode launch from the committed rocprofv3 PMC measurement
-    (tools/pmc_traffic.py -> profiles/*_pmc_traffic.json), scaled to N stripes; None if no
-    measurement exists for this geometry."""
+def pmc_traffic(k, m, C, N, kernel_kind, pad):
+    """HBM bytes per encode launch from the committed rocprofv3 PMC measurement of the same
+    geometry and layout (tools/pmc_traffic.py -> profiles/*_pmc_traffic.json), scaled to N
+    stripes; (None, None) when no measurement of this exact configuration exists."""
     import glob
 
     prefix = "void lsec::k_gf8_bytewise<%d," % m if kernel_kind == 1 else "void lsec::k_gf8_bitsliced<%d," % m
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
         with open(f) as fh:
             d = json.load(fh)
-        if (d.get("k"), d.get("m"), d.get("chunk")) != (k, m, C):
+        if (d.get("k"), d.get("m"), d.get("chunk"), d.get("pad", 1024)) != (k, m, C, pad):
             continue
         for name, v in d["kernels"].items():
             if name.startswith(prefix):
@@ -122,11 +162,11 @@ def pmc_traffic(k, m, C, N, kernel_kind):
     return None, None
 
 
-def host_path_rate(L, plan, k, m, C, lost, nstripes, pinned=False, reps=3):
+def host_path_rate(plan, k, m, C, lost, nstripes, pinned=False, reps=3):
     """et_encode_stripes / et_decode_stripes from host memory (PCIe-inclusive), median of reps.
 
-    pinned=False: pageable numpy buffers (LStore's cache pages) -> packed into the engine's
-    pinned staging -> H2D -> kernel -> D2H -> unpacked.  pinned=True: page-locked buffers
+    pinned=False: pageable numpy buffers (LStore's cache pages) -> pinned in place or packed
+    into the engine's pinned staging -> H2D -> kernel -> D2H.  pinned=True: page-locked buffers
     (torch pin_memory = hipHostMalloc), DMA'd in place with no host copies."""
     if pinned:
         import torch
@@ -155,202 +195,270 @@ def host_path_rate(L, plan, k, m, C, lost, nstripes, pinned=False, reps=3):
                      "pageable host buffers -> pinned staging -> H2D -> kernel -> D2H -> host")}
 
 
-def main():
-    a = parse()
-    import torch
-    import torch.distributed as dist
+# ----------------------------------------------------------------------------- the engine
+class HipEngine:
+    """The device-resident hot path: liblstore_ec.so's lsec_encode_dev / lsec_decode_dev on
+    HBM-resident stripes, timed with HIP events on the launch stream."""
 
-    import lstore_amd as L
-    from lstore_amd import erasure as E
+    def __init__(self, a, rank, world, local):
+        import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        # one process per GPU; the only collectives are the timing barrier and the max-over-ranks
-        # reduction (RCCL by default; LSEC_DIST_BACKEND=gloo lets ranks share one GPU for rehearsal)
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        import lstore_amd as L
+        from lstore_amd import erasure as E
+
+        self.torch, self.L, self.E, self.a = torch, L, E, a
         torch.cuda.set_device(local % torch.cuda.device_count())
-        backend = os.environ.get("LSEC_DIST_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+        self.dev = torch.device("cuda", torch.cuda.current_device())
+        self.backend = os.environ.get("LSEC_DIST_BACKEND", "nccl") if world > 1 else None
+        bw_v, bs_v = (int(x) for x in a.variant.split(","))
+        E.set_kernel_variant(bw_v, bs_v)
+        self.method = E.JE_METHOD_NAMES.index(a.method)
+        self.plan = L.Plan.for_chunk(self.method, a.k, a.m, a.chunk)
+        self.P = self.plan.packet_size
+        self.kernel = self.plan.kernel
+        self.stream = torch.cuda.current_stream()
+        self.sh = self.stream.cuda_stream
+        self.er = E._erasure_array([a.lost])
+        self.plan.prepare_decode([a.lost])
+        self.lib = E.lib()
+        self.tensors = None
+
+    def init_dist(self, dist):
+        if self.backend == "nccl":
+            dist.init_process_group("nccl", device_id=self.dev)
         else:
-            dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
-    bw_v, bs_v = (int(x) for x in a.variant.split(","))
-    E.set_kernel_variant(bw_v, bs_v)
+            dist.init_process_group(self.backend)
 
-    method = E.JE_METHOD_NAMES.index(a.method)
-    k, m, C, N = a.k, a.m, a.chunk, a.stripes
-    if a.total_stripes > 0:
-        from lstore_amd.partition import stripe_range
-        s0, s1 = stripe_range(a.total_stripes, world, rank)
-        N = max(1, s1 - s0)
-    plan = L.Plan.for_chunk(method, k, m, C)
-    P = plan.packet_size
+    def reduce_device(self, dist):
+        return self.dev if dist.get_backend() == "nccl" else None
 
-    stream = torch.cuda.current_stream()
-    sh = stream.cuda_stream
-    er = E._erasure_array([a.lost])
-    plan.prepare_decode([a.lost])
-    lib = E.lib()
-
-    def workload(pad, seed):
+    def workload(self, N, pad, seed, first=0):
         """Synthetic stripes resident in HBM: data [N][k][C], parity [N][m][C] and the rebuilt
-        shard [N][1][C], every shard row followed by `pad` unused bytes (the device-resident
-        layout).  Returns the tensors and the encode / decode launchers."""
-        g = torch.Generator(device=dev).manual_seed(seed)
-        data = torch.randint(0, 256, (N, k, C + pad), dtype=torch.uint8, device=dev, generator=g)[:, :, :C]
-        par = torch.empty((N, m, C + pad), dtype=torch.uint8, device=dev)[:, :, :C]
-        rebuilt = torch.empty((N, 1, C + pad), dtype=torch.uint8, device=dev)[:, :, :C]
+        shard [N][1][C], every shard row followed by `pad` unused bytes.  Returns the encode /
+        decode launchers (the tensors stay referenced until drop())."""
+        torch, a, plan, lib, E = self.torch, self.a, self.plan, self.lib, self.E
+        k, m, C = a.k, a.m, a.chunk
+        g = torch.Generator(device=self.dev).manual_seed(seed)
+        data = torch.randint(0, 256, (N, k, C + pad), dtype=torch.uint8, device=self.dev, generator=g)[:, :, :C]
+        par = torch.empty((N, m, C + pad), dtype=torch.uint8, device=self.dev)[:, :, :C]
+        rebuilt = torch.empty((N, 1, C + pad), dtype=torch.uint8, device=self.dev)[:, :, :C]
         enc_refs, _, _ = plan.tensor_refs(data, par)
         enc_arr = plan.shard_refs(enc_refs)
         dec_refs = list(enc_refs)
         dec_refs[a.lost] = (rebuilt.data_ptr(), rebuilt.stride(0))
         dec_arr = plan.shard_refs(dec_refs)
+        self.tensors = (data, par, rebuilt)
 
         def encode():
-            rc = lib.lsec_encode_dev(plan.ptr, enc_arr, N, C, sh)
-            if rc:
+            if lib.lsec_encode_dev(plan.ptr, enc_arr, N, C, self.sh):
                 raise E.ErasureError(E.last_error())
 
         def decode():
-            rc = lib.lsec_decode_dev(plan.ptr, dec_arr, N, C, er, sh)
-            if rc:
+            if lib.lsec_decode_dev(plan.ptr, dec_arr, N, C, self.er, self.sh):
                 raise E.ErasureError(E.last_error())
 
-        return data, par, rebuilt, encode, decode
+        return encode, decode
 
-    def launch_times(encode, decode, reps):
+    def drop(self):
+        self.tensors = None
+        self.torch.cuda.empty_cache()
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def launch_times(self, encode, decode, reps):
         """average encode / decode launch time (s), HIP events on the launch stream"""
+        torch = self.torch
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-        ev[0].record(stream)
+        ev[0].record(self.stream)
         for _ in range(reps):
             encode()
-        ev[1].record(stream)
+        ev[1].record(self.stream)
         for _ in range(reps):
             decode()
-        ev[2].record(stream)
+        ev[2].record(self.stream)
         torch.cuda.synchronize()
         return ev[0].elapsed_time(ev[1]) / 1e3 / reps, ev[1].elapsed_time(ev[2]) / 1e3 / reps
 
-    data, par, rebuilt, encode, decode = workload(a.pad, 1234 + rank)
+    def check(self, N):
+        """Bit-exact parity of sampled stripes against the reference itself (oracle/_ref:
+        vendor/jerasure), or the restatement when _ref is not built; the rebuilt shard must
+        equal the lost one."""
+        import oracle as O
+
+        a = self.a
+        data, par, rebuilt = self.tensors
+        pick = sorted({0, N // 2, N - 1})
+        hd, hp, hr = data[pick].cpu().numpy(), par[pick].cpu().numpy(), rebuilt[pick].cpu().numpy()
+        ref = O.RefPlan(self.method, a.k, a.m, 8, self.P) if O.ref_available() else None
+        ok = True
+        for i in range(len(pick)):
+            want = ref.encode(hd[i]) if ref else O.encode(self.method, hd[i], a.m, self.P)
+            ok &= bool(np.array_equal(want, hp[i]))
+            ok &= bool(np.array_equal(hr[i, 0], np.vstack([hd[i], hp[i]])[a.lost]))
+        if ref:
+            ref.close()
+        return ok, ("bit-exact vs oracle/_ref (vendor/jerasure) on stripes %s" % pick if ref else
+                    "bit-exact vs the oracle restatement on stripes %s (_ref not built)" % pick)
+
+    def extras(self, N, t_enc, t_dec, rank, world):
+        """rank-0, N = 1 extras: the padded layout A/B, the HBM copy probe, the CPU reference
+        and the PCIe-inclusive host path."""
+        a, torch, lib, E = self.a, self.torch, self.lib, self.E
+        k, m, C = a.k, a.m, a.chunk
+        out = {}
+        enc_hbm, dec_hbm, data_bytes = (k + m) * C * N, (k + 1) * C * N, k * C * N
+        reps = max(3, min(10, a.steps))
+        layout = {"shard_pad_bytes": a.pad}
+        if world == 1 and not a.no_layout_ab:
+            # the same stripes with a 1 KiB pad after every shard row (or, when the headline is
+            # padded, unpadded), launch-timed beside the headline layout for the record
+            alt = 1024 if a.pad == 0 else 0
+            self.drop()
+            enc0, dec0 = self.workload(N, alt, 1234 + rank)
+            enc0()
+            dec0()
+            te0, td0 = self.launch_times(enc0, dec0, reps)
+            layout["padded" if alt else "unpadded"] = {
+                "shard_pad_bytes": alt, "encode_frac": round(enc_hbm / te0 / HBM_PEAK, 4),
+                "decode_frac": round(dec_hbm / td0 / HBM_PEAK, 4),
+                "value_from_launch_times": round(data_bytes / (te0 + td0) / 2**30, 2),
+                "headline_value_from_launch_times": round(data_bytes / (t_enc + t_dec) / 2**30, 2)}
+            del enc0, dec0
+        out["layout"] = layout
+        self.drop()
+        if world == 1 and not a.no_copy_ref:
+            # the box's practical HBM ceiling beside the spec peak: streaming device copies of the
+            # encode launch's byte count (half read, half written), HIP events on the launch stream --
+            # the engine's probe kernel (lsec_hbm_copy_dev: the coding kernels' memory shape) and torch's copy_
+            nb = enc_hbm // 2
+            src = torch.empty(nb, dtype=torch.uint8, device=self.dev)
+            dst = torch.empty_like(src)
+
+            def probe():
+                if lib.lsec_hbm_copy_dev(dst.data_ptr(), src.data_ptr(), nb, self.sh):
+                    raise E.ErasureError(E.last_error())
+
+            def timed(fn):
+                fn()
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                ev[0].record(self.stream)
+                for _ in range(reps):
+                    fn()
+                ev[1].record(self.stream)
+                torch.cuda.synchronize()
+                return ev[0].elapsed_time(ev[1]) / 1e3 / reps
+
+            t_probe, t_torch = timed(probe), timed(lambda: dst.copy_(src))
+            out["hbm_copy_ref"] = {
+                "what": "device->device copy of (k+m)*C*N/2 bytes, read+write counted",
+                "probe_GBps": round(2 * nb / t_probe / 1e9, 1), "probe_frac": round(2 * nb / t_probe / HBM_PEAK, 4),
+                "torch_copy_GBps": round(2 * nb / t_torch / 1e9, 1),
+                "encode_vs_probe": round((enc_hbm / t_enc) / (2 * nb / t_probe), 3),
+                "decode_vs_probe": round((dec_hbm / t_dec) / (2 * nb / t_probe), 3)}
+            del src, dst
+            self.drop()
+        if rank == 0 and world == 1:
+            # the reference CPU path is timed at N=1 only (at N>1 it would only delay the ranks' exit)
+            out["cpu_baseline"] = None if a.no_cpu else cpu_baseline(self.method, k, m, C, self.P, a.lost, a.cpu_seconds)
+            if not a.no_host_path:
+                ns = max(8, min(256, (4 << 30) // ((k + m) * C)))
+                host = host_path_rate(self.plan, k, m, C, a.lost, ns)
+                host["pinned"] = host_path_rate(self.plan, k, m, C, a.lost, ns, pinned=True)
+                out["host_path"] = host
+        return out
+
+    def kernel_name(self):
+        return "gf8_bytewise (encode)" if self.kernel == 1 else "gf8_bitsliced (encode)"
+
+    def traffic(self, N):
+        return pmc_traffic(self.a.k, self.a.m, self.a.chunk, N, self.kernel, self.a.pad)
+
+    def close(self):
+        self.drop()
+        self.plan.close()
+
+
+# ----------------------------------------------------------------------------- one rank
+def run_rank(a, rank, world, local, engine_cls=HipEngine):
+    """One rank of the benchmark (also what tests/test_multirank.py runs over gloo with a CPU
+    engine).  Returns rank 0's JSON dict (None on other ranks)."""
+    import torch.distributed as dist
+
+    from lstore_amd.partition import max_over_ranks, stripe_range
+
+    eng = engine_cls(a, rank, world, local)
+    if world > 1:
+        # one process per GPU; the only collectives are the timing barrier, the max-over-ranks
+        # reduction and the gather of per-rank figures (RCCL by default)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        eng.init_dist(dist)
+    k, m, C, N = a.k, a.m, a.chunk, a.stripes
+    first = rank * N  # global index of this rank's first stripe
+    if a.total_stripes > 0:
+        first, s1 = stripe_range(a.total_stripes, world, rank)
+        N = s1 - first
+        if N <= 0:
+            raise SystemExit(f"rank {rank}: --total-stripes {a.total_stripes} leaves no stripes for {world} ranks")
+    encode, decode = eng.workload(N, a.pad, 1234 + rank, first)
 
     for _ in range(a.warmup):
         encode()
         decode()
-    torch.cuda.synchronize()
+    eng.sync()
 
     # ---- timed region: K steps, barrier + synchronize on both sides
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    eng.sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         encode()
         decode()
-    torch.cuda.synchronize()
+    eng.sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        from lstore_amd.partition import max_over_ranks
-        elapsed = max_over_ranks(elapsed, dev if dist.get_backend() == "nccl" else None)
+        elapsed = max_over_ranks(elapsed, eng.reduce_device(dist))
 
-    # ---- per-kernel timing with HIP events on the launch stream (roofline)
+    # ---- per-kernel timing on the launch stream (roofline), on every rank
     reps = max(3, min(10, a.steps))
-    t_enc, t_dec = launch_times(encode, decode, reps)
+    t_enc, t_dec = eng.launch_times(encode, decode, reps)
 
-    # ---- parity check (bit-exact vs the CPU oracle on sampled stripes)
-    import oracle as O
-
-    ok = True
-    pick = sorted({0, N // 2, N - 1})
-    hd = data[pick].cpu().numpy()
-    hp = par[pick].cpu().numpy()
-    hr = rebuilt[pick].cpu().numpy()
-    for i in range(len(pick)):
-        ref = O.encode(method, hd[i], m, P)
-        ok &= bool(np.array_equal(ref, hp[i]))
-        ok &= bool(np.array_equal(hr[i, 0], np.vstack([hd[i], hp[i]])[a.lost]))
-    if not ok:
-        print(json.dumps({"error": "parity mismatch vs oracle", "rank": rank}), flush=True)
-        sys.exit(1)
-
+    # ---- parity check (bit-exact vs the reference on sampled stripes), on every rank
+    ok, parity_note = eng.check(N)
     data_bytes = k * C * N
     enc_hbm = (k + m) * C * N
     dec_hbm = (k + 1) * C * N
-    layout = {"shard_pad_bytes": a.pad}
-    if a.pad and world == 1 and not a.no_layout_ab:
-        # the same stripes in the unpadded layout (shards exactly C apart, as one cache page
-        # holds them), launch-timed beside the padded one for the record
-        del data, par, rebuilt
-        torch.cuda.empty_cache()
-        _, _, _, enc0, dec0 = workload(0, 1234 + rank)
-        enc0()
-        dec0()
-        te0, td0 = launch_times(enc0, dec0, reps)
-        layout["unpadded"] = {"encode_frac": round(enc_hbm / te0 / HBM_PEAK, 4),
-                              "decode_frac": round(dec_hbm / td0 / HBM_PEAK, 4),
-                              "value_from_launch_times": round(data_bytes / (te0 + td0) / 2**30, 2),
-                              "padded_value_from_launch_times": round(data_bytes / (t_enc + t_dec) / 2**30, 2)}
-        del enc0, dec0
-        torch.cuda.empty_cache()
-    copy_ref = None
-    if world == 1 and not a.no_copy_ref:
-        # the box's practical HBM ceiling beside the spec peak: streaming device copies of the
-        # encode launch's byte count (half read, half written), HIP events on the launch stream --
-        # the engine's probe kernel (lsec_hbm_copy_dev: the coding kernels' memory shape) and torch's copy_
-        data = par = rebuilt = None
-        torch.cuda.empty_cache()
-        nb = enc_hbm // 2
-        src = torch.empty(nb, dtype=torch.uint8, device=dev)
-        dst = torch.empty_like(src)
+    mine = {"rank": rank, "stripes": N, "parity_ok": ok,
+            "encode_gibps": round(data_bytes / t_enc / 2**30, 2), "decode_gibps": round(data_bytes / t_dec / 2**30, 2),
+            "encode_frac": round(enc_hbm / t_enc / HBM_PEAK, 4), "decode_frac": round(dec_hbm / t_dec / HBM_PEAK, 4),
+            "avg_encode_launch_ms": round(t_enc * 1e3, 4), "avg_decode_launch_ms": round(t_dec * 1e3, 4)}
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+    else:
+        per_rank = [mine]
+    if not all(r["parity_ok"] for r in per_rank):
+        if rank == 0:
+            print(json.dumps({"error": "parity mismatch vs reference", "per_rank": per_rank}), flush=True)
+        raise SystemExit(1)
 
-        def probe():
-            if lib.lsec_hbm_copy_dev(dst.data_ptr(), src.data_ptr(), nb, sh):
-                raise E.ErasureError(E.last_error())
-
-        def timed(fn):
-            fn()
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-            ev[0].record(stream)
-            for _ in range(reps):
-                fn()
-            ev[1].record(stream)
-            torch.cuda.synchronize()
-            return ev[0].elapsed_time(ev[1]) / 1e3 / reps
-
-        t_probe, t_torch = timed(probe), timed(lambda: dst.copy_(src))
-        copy_ref = {"what": "device->device copy of (k+m)*C*N/2 bytes, read+write counted",
-                    "probe_GBps": round(2 * nb / t_probe / 1e9, 1), "probe_frac": round(2 * nb / t_probe / HBM_PEAK, 4),
-                    "torch_copy_GBps": round(2 * nb / t_torch / 1e9, 1),
-                    "encode_vs_probe": round((enc_hbm / t_enc) / (2 * nb / t_probe), 3),
-                    "decode_vs_probe": round((dec_hbm / t_dec) / (2 * nb / t_probe), 3)}
-        del src, dst
-        torch.cuda.empty_cache()
+    extras = eng.extras(N, t_enc, t_dec, rank, world)
     if a.total_stripes > 0:
         value = k * C * a.total_stripes * a.steps / elapsed / 2**30
     else:
         value = data_bytes * world * a.steps / elapsed / 2**30
     achieved = enc_hbm / t_enc
-    traffic, traffic_src = pmc_traffic(k, m, C, N, plan.kernel)
+    traffic, traffic_src = eng.traffic(N)
 
     out = None
     if rank == 0:
-        # the reference CPU path is timed at N=1 only (one process; at N>1 it would only delay the ranks' exit)
-        cpu = None if (a.no_cpu or world > 1) else cpu_baseline(method, k, m, C, P, a.lost, a.cpu_seconds)
-        host = None
-        if not a.no_host_path and world == 1:
-            ns = max(8, min(256, (4 << 30) // ((k + m) * C)))
-            host = host_path_rate(L, plan, k, m, C, a.lost, ns)
-            host["pinned"] = host_path_rate(L, plan, k, m, C, a.lost, ns, pinned=True)
+        method = a.method
         out = {
-            "metric": "erasure encode+decode GiB/s (device-resident), RS(6+3) 1 MiB stripes"
-            if (method, k, m, C) == (0, 6, 3, 1 << 20) else
-            f"erasure encode+decode GiB/s (device-resident), {a.method}({k}+{m}) {C} B chunks",
+            "metric": HEADLINE if (method, k, m, C) == ("reed_sol_van", 6, 3, 1 << 20) else
+            f"erasure encode+decode GiB/s (device-resident), {method}({k}+{m}) {C} B chunks",
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -362,30 +470,87 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (torch.randint bytes, resident in HBM)",
-            "config": {"workload": f"{a.method}({k}+{m}) encode + decode(lost shard {a.lost}), C={C} B per shard, "
+            "config": {"workload": f"{method}({k}+{m}) encode + decode(lost shard {a.lost}), C={C} B per shard, "
                                    f"{N} stripes/GPU, k*C={k * C} B user data per stripe",
-                       "method": a.method, "k": k, "m": m, "chunk_bytes": C, "packet_size": P,
-                       "stripes_per_gpu": N, "lost_shard": a.lost, "parallelism": f"static stripe partition x{world}"},
+                       "method": method, "k": k, "m": m, "chunk_bytes": C, "packet_size": eng.P,
+                       "stripes_per_gpu": N, "lost_shard": a.lost, "shard_pad_bytes": a.pad,
+                       "parallelism": f"static stripe partition x{world}"},
             "encode_gibps": round(data_bytes / t_enc / 2**30, 2),
             "decode_gibps": round(data_bytes / t_dec / 2**30, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "gf8_bytewise (encode)" if plan.kernel == 1 else "gf8_bitsliced (encode)",
+                         "kernel": eng.kernel_name(),
                          "algorithmic_bytes_per_launch": enc_hbm, "avg_launch_ms": round(t_enc * 1e3, 4),
                          "decode_achieved_GBps": round(dec_hbm / t_dec / 1e9, 1),
                          "decode_frac": round(dec_hbm / t_dec / HBM_PEAK, 4)},
-            "layout": layout,
-            "hbm_copy_ref": copy_ref,
-            "cpu_baseline": cpu,
-            "host_path": host,
-            "parity_check": "bit-exact vs oracle on stripes %s" % pick,
+            "per_rank": per_rank,
+            "layout": extras.get("layout"),
+            "hbm_copy_ref": extras.get("hbm_copy_ref"),
+            "cpu_baseline": extras.get("cpu_baseline"),
+            "host_path": extras.get("host_path"),
+            "parity_check": parity_note,
         }
-        print(json.dumps(out), flush=True)
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    plan.close()
+    eng.close()
+    return out
+
+
+# ----------------------------------------------------------------------------- launching
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawned(rank, a, world, port, engine_cls):
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    run_rank(a, rank, world, rank, engine_cls)
+
+
+def launch(a, engine_cls=HipEngine):
+    """Run the benchmark on a.gpus ranks; returns the process exit code."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if a.gpus < 1:
+        print(json.dumps({"error": f"--gpus {a.gpus} < 1"}), flush=True)
+        return 2
+    if env_world is not None:
+        world = int(env_world)
+        if world != a.gpus:
+            print(json.dumps({"error": f"WORLD_SIZE={world} but --gpus {a.gpus}: launch one rank per GPU"}), flush=True)
+            return 2
+        run_rank(a, int(os.environ.get("RANK", "0")), world, int(os.environ.get("LOCAL_RANK", "0")), engine_cls)
+        return 0
+    if a.gpus == 1:
+        run_rank(a, 0, 1, 0, engine_cls)
+        return 0
+    # self-launch: N ranks, one process per GPU, spawned before this process touches the GPU
+    import torch.multiprocessing as mp
+
+    ctx = mp.start_processes(_spawned, args=(a, a.gpus, _free_port(), engine_cls), nprocs=a.gpus,
+                             join=False, start_method="spawn")
+    try:
+        while not ctx.join():
+            pass
+    except mp.ProcessRaisedException as e:
+        print(json.dumps({"error": "a rank failed", "detail": str(e)[-2000:]}), flush=True)
+        return 1
+    except mp.ProcessExitedException as e:
+        print(json.dumps({"error": "a rank exited", "detail": str(e)[-2000:]}), flush=True)
+        return 1
+    return 0
+
+
+def main():
+    sys.exit(launch(parse()))
 
 
 if __name__ == "__main__":

@@ -278,12 +278,16 @@ int fp_form_encoding(lio_erasure_plan_t *p) {
 
 int fp_form_decoding(lio_erasure_plan_t *p) {
   if (!p) return -1;
+  // "Already formed so skip step": every *_form_coding_matrix returns 0 at once when its
+  // matrix (Cauchy) or bitmatrix (liberation family) exists (erasure_tools.c:137, :152, :169,
+  // :184, :198), whatever the schedule
+  const bool cauchy = p->method == CAUCHY_ORIG || p->method == CAUCHY_GOOD;
+  const bool formed = cauchy ? p->encode_matrix != nullptr : liberation_family(p->method) && p->encode_bitmatrix != nullptr;
   const int rc = form_matrices(p, false);
-  if (rc) return rc;
-  // cauchy_*_form_coding_matrix / liberation family return -1 while the schedule is
-  // still unset (erasure_tools.c:142, :159, :176, :190, :204)
-  if (p->method != REED_SOL_VAN && p->method != REED_SOL_R6_OP && p->method != RAID4 && !p->encode_schedule)
-    return -1;
+  if (rc || formed) return rc;
+  // ... and -1 when it has just formed it while the schedule is still unset (:142, :159,
+  // :176, :190, :204)
+  if ((cauchy || liberation_family(p->method)) && !p->encode_schedule) return -1;
   return 0;
 }
 
@@ -781,28 +785,45 @@ bool inplace_overlaps_locked(uintptr_t lo, uintptr_t hi) {
   return false;
 }
 
-bool pinned_layout(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids) {
+// Caller page-locked buffers.  pinned: every staged chunk of the first and last stripe is
+// page-locked (a stray pageable chunk in between stays correct -- hipMemcpyAsync accepts
+// pageable memory too, only slower).  by_kernel (asked with kernel_ok): small runs, and EVERY
+// chunk checked to have a device address -- see caller_pinned_aliases.  The whole decision is
+// one pass under g_inplace_mu, with every chunk's page range checked against the in-flight
+// in-place registrations first: a range a concurrent InPlacePin has claimed (it claims before
+// it registers and releases after it unregisters) is never taken for caller-pinned memory,
+// since its owner may unregister it while this call's DMA or copy kernel still reads it.
+bool caller_pinned_aliases(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids,
+                           const std::vector<int> &out_ids, long long C, std::vector<uint64_t> &dev);
+
+struct CallerPinned {
+  bool pinned = false, by_kernel = false;
+  std::vector<uint64_t> dev;  // by_kernel: device address of every chunk (caller_pinned_aliases order)
+};
+
+CallerPinned caller_pinned(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
+                           long long C, bool kernel_ok) {
   static const bool off = getenv("LSEC_NO_PINNED_DMA") != nullptr;
-  if (off) return false;
-  // held across the attribute queries too: a registration claimed after the overlap scan
-  // must not be seen as caller-pinned
+  CallerPinned r;
+  if (off) return r;
   std::lock_guard<std::mutex> lk(g_inplace_mu);
   if (!g_inplace.empty()) {
-    for (int s = 0; s < nstripes; ++s) {
+    for (int s = 0; s < nstripes; ++s)
       for (const std::vector<int> *ids : {&in_ids, &out_ids})
         for (int id : *ids) {
-          const uintptr_t a = reinterpret_cast<uintptr_t>(ptrs[static_cast<size_t>(s) * km + id]) & ~(kPage - 1);
-          if (inplace_overlaps_locked(a, a + kPage)) return false;
+          const uintptr_t a = reinterpret_cast<uintptr_t>(ptrs[static_cast<size_t>(s) * km + id]);
+          if (inplace_overlaps_locked(a & ~(kPage - 1), (a + static_cast<uintptr_t>(C) + kPage - 1) & ~(kPage - 1))) return r;
         }
-    }
   }
   for (int s : {0, nstripes - 1}) {
     for (int id : in_ids)
-      if (!is_pinned_host(ptrs[static_cast<size_t>(s) * km + id])) return false;
+      if (!is_pinned_host(ptrs[static_cast<size_t>(s) * km + id])) return r;
     for (int id : out_ids)
-      if (!is_pinned_host(ptrs[static_cast<size_t>(s) * km + id])) return false;
+      if (!is_pinned_host(ptrs[static_cast<size_t>(s) * km + id])) return r;
   }
-  return true;
+  r.pinned = true;
+  r.by_kernel = kernel_ok && caller_pinned_aliases(ptrs, nstripes, km, in_ids, out_ids, C, r.dev);
+  return r;
 }
 
 // Pageable caller buffers of a large batch are pinned in place for the duration of the call
@@ -987,6 +1008,7 @@ bool kernel_transport_aligned(char **ptrs, int nstripes, int km, const std::vect
 // (a pageable chunk between pinned ones is harmless to a DMA but would fault a kernel).  The
 // check costs ~0.06 us per chunk (tools/probes/pinned_attr_probe.cpp).  dev[i] gets the device
 // address of chunk i, in the order stripe, then in_ids, then out_ids.
+// (called by caller_pinned with g_inplace_mu held)
 bool caller_pinned_aliases(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids,
                            const std::vector<int> &out_ids, long long C, std::vector<uint64_t> &dev) {
   size_t runs = 0, total = 0;
@@ -1107,12 +1129,12 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   InPlacePin inplace;
   const KernelCopy kpol = kernel_copy_policy();
   const bool aligned = kpol != KernelCopy::kNever && kernel_transport_aligned(ptrs, nstripes, km, in_ids, out_ids, C, cb);
-  const bool caller_pinned = pinned_layout(ptrs, nstripes, km, in_ids, out_ids);
+  CallerPinned cp = caller_pinned(ptrs, nstripes, km, in_ids, out_ids, C, aligned);
+  const bool caller_pinned = cp.pinned;
   const bool pinned =
       caller_pinned || inplace.pin(ptrs, nstripes, km, in_ids, out_ids, C, aligned && kpol == KernelCopy::kAll);
-  std::vector<uint64_t> calias;  // caller-pinned chunks moved by kernel: their device addresses
-  const bool caller_by_kernel =
-      caller_pinned && aligned && caller_pinned_aliases(ptrs, nstripes, km, in_ids, out_ids, C, calias);
+  const std::vector<uint64_t> &calias = cp.dev;  // caller-pinned chunks moved by kernel: their device addresses
+  const bool caller_by_kernel = cp.by_kernel;
   const size_t nio = in_ids.size() + out_ids.size();
   // device address of byte c0 of chunk (stripe s, list position i: inputs, then outputs)
   const auto dev_at = [&](int s, size_t i, int id, long long c0) -> uint64_t {
@@ -1295,11 +1317,18 @@ bool is_device_ptr(const void *ptr) {
 }
 
 // all k+m pointers of every stripe device memory?  then describe them as shard refs
-bool device_layout(const lio_erasure_plan_t *p, char **ptrs, int nstripes, std::vector<lsec_shard_t> &sh) {
+// Returns 1 (device layout in sh), 0 (host memory), -1 (device and host pointers mixed in the
+// first or last stripe, or an irregular device stride: refused rather than guessed).
+int device_layout(const lio_erasure_plan_t *p, char **ptrs, int nstripes, std::vector<lsec_shard_t> &sh) {
   const int km = p->data_strips + p->parity_strips;
-  if (!is_device_ptr(ptrs[0])) return false;
-  for (int i = 1; i < km; ++i)
-    if (!is_device_ptr(ptrs[i])) return false;
+  int ndev = 0;
+  for (int s : {0, nstripes - 1}) {
+    for (int i = 0; i < km; ++i) ndev += is_device_ptr(ptrs[static_cast<size_t>(s) * km + i]);
+    if (nstripes == 1) break;
+  }
+  const int total = nstripes == 1 ? km : 2 * km;
+  if (ndev == 0) return 0;
+  if (ndev != total) return fail("stripe pointers mix device and host memory");
   sh.resize(km);
   for (int i = 0; i < km; ++i) {
     sh[i].base = ptrs[i];
@@ -1307,8 +1336,9 @@ bool device_layout(const lio_erasure_plan_t *p, char **ptrs, int nstripes, std::
   }
   for (int s = 2; s < nstripes; ++s)  // require a regular stride (one layout descriptor)
     for (int i = 0; i < km; ++i)
-      if (ptrs[static_cast<size_t>(s) * km + i] != ptrs[i] + s * sh[i].stride) return false;
-  return true;
+      if (ptrs[static_cast<size_t>(s) * km + i] != ptrs[i] + s * sh[i].stride)
+        return fail("device stripe pointers are not regularly strided (stripe %d, shard %d)", s, i);
+  return 1;
 }
 
 hipStream_t thread_stream() {
@@ -1637,10 +1667,12 @@ int run_coalesced(PlanExt *e, char **ptrs, int nstripes, long long C, const std:
   r.kind = kind;
   r.packet = e->pub.packet_size;
   r.w = e->pub.w;
-  r.pinned = pinned_layout(ptrs, nstripes, r.km, in_ids, out_ids);
-  r.by_kernel = r.pinned && kernel_copy_policy() != KernelCopy::kNever &&
-                kernel_transport_aligned(ptrs, nstripes, r.km, in_ids, out_ids, C, C) &&
-                caller_pinned_aliases(ptrs, nstripes, r.km, in_ids, out_ids, C, r.dev);
+  CallerPinned cp = caller_pinned(ptrs, nstripes, r.km, in_ids, out_ids, C,
+                                  kernel_copy_policy() != KernelCopy::kNever &&
+                                      kernel_transport_aligned(ptrs, nstripes, r.km, in_ids, out_ids, C, C));
+  r.pinned = cp.pinned;
+  r.by_kernel = cp.by_kernel;
+  r.dev.swap(cp.dev);
   return Dispatcher::for_device(dev)->run(r);
 }
 
@@ -1651,6 +1683,51 @@ int run_host_auto(PlanExt *e, char **ptrs, int nstripes, long long C, const std:
   const size_t bytes = static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()) * C;
   if (bytes <= coalesce_limit()) return run_coalesced(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
   return run_host(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
+}
+
+// Last resort of the per-stripe fn-pointers after a failed call (a pinned allocation or a
+// registration refused, a dispatcher error): plain synchronous copies of the caller's chunks
+// into per-thread device scratch, the kernel, and synchronous copies back -- no page-locked
+// memory, no dispatcher, no kernel transport.  Still the GPU kernels: there is no CPU path.
+int run_direct(PlanExt *e, char **ptrs, long long C, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
+               const void *image, int kind) {
+  struct Scratch {
+    int dev = -1;
+    char *d = nullptr;
+    size_t cap = 0;
+    ~Scratch() {
+      if (d) (void)hipFree(d);
+    }
+  };
+  static thread_local Scratch sc;
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  const size_t nin = in_ids.size(), nout = out_ids.size(), need = (nin + nout) * static_cast<size_t>(C);
+  if (sc.dev != dev || sc.cap < need) {
+    if (sc.d) {
+      (void)hipSetDevice(sc.dev);
+      (void)hipFree(sc.d);
+      (void)hipSetDevice(dev);
+    }
+    sc.d = nullptr;
+    sc.cap = 0;
+    sc.dev = dev;
+    HIP_OK(hipMalloc(&sc.d, need));
+    sc.cap = need;
+  }
+  hipStream_t st = thread_stream();
+  if (!st) return fail("no HIP stream");
+  ShardRef in[lsec::kMaxK], out[kMaxM];
+  for (size_t j = 0; j < nin; ++j) {
+    HIP_OK(hipMemcpyAsync(sc.d + j * C, ptrs[in_ids[j]], C, hipMemcpyHostToDevice, st));
+    in[j] = {reinterpret_cast<uint64_t>(sc.d) + j * C, 0};
+  }
+  for (size_t r = 0; r < nout; ++r) out[r] = {reinterpret_cast<uint64_t>(sc.d) + (nin + r) * C, 0};
+  if (enqueue_apply(kind, image, static_cast<int>(nin), static_cast<int>(nout), in, out, 1, C, e->pub.packet_size, st, e->pub.w))
+    return -1;
+  for (size_t r = 0; r < nout; ++r) HIP_OK(hipMemcpyAsync(ptrs[out_ids[r]], sc.d + (nin + r) * C, C, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  return 0;
 }
 
 // ---------------------------------------------------------------- host-path device set
@@ -1716,7 +1793,9 @@ int encode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C) {
   if (check_geometry(p, C)) return -1;
   if (nstripes <= 0 || C == 0) return 0;
   std::vector<lsec_shard_t> sh;
-  if (device_layout(p, ptrs, nstripes, sh)) {
+  const int dl = device_layout(p, ptrs, nstripes, sh);
+  if (dl < 0) return -1;
+  if (dl) {
     hipStream_t st = thread_stream();
     if (!st) return fail("no HIP stream");
     if (encode_dev(e, sh.data(), nstripes, C, st)) return -1;
@@ -1747,7 +1826,9 @@ int decode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C, cons
   if (p->method == RAID4 && ids[0] >= p->data_strips) return 0;
   if (nstripes <= 0 || C == 0) return 0;
   std::vector<lsec_shard_t> sh;
-  if (device_layout(p, ptrs, nstripes, sh)) {
+  const int dl = device_layout(p, ptrs, nstripes, sh);
+  if (dl < 0) return -1;
+  if (dl) {
     hipStream_t st = thread_stream();
     if (!st) return fail("no HIP stream");
     if (decode_dev(e, sh.data(), nstripes, C, erasures, st)) return -1;
@@ -1827,22 +1908,68 @@ int magic_dev_impl(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C
 }
 
 // plan->encode_block / plan->decode_block
+// Retry of a failed host-memory fn-pointer call through run_direct.  Geometry errors are not
+// retried (they would fail again); a plan from et_generate_plan never has them.
+int retry_direct(PlanExt *e, char **ptr, long long C, const std::vector<int> &ids) {
+  const std::string first = tl_err;
+  lio_erasure_plan_t *p = &e->pub;
+  if (check_geometry(p, C) != 0) return -1;
+  std::vector<lsec_shard_t> sh;
+  if (device_layout(p, ptr, 1, sh) != 0) {
+    tl_err = first;  // device pointers (or mixed): nothing to retry with another transport
+    return -1;
+  }
+  int rc;
+  if (ids.empty()) {  // encode
+    const int k = p->data_strips;
+    const void *cells = nullptr;
+    rc = encode_cells(e, &cells);
+    if (rc == 0) {
+      const int R = encode_rows(e);
+      std::vector<int> in_ids(k), out_ids(R);
+      for (int j = 0; j < k; ++j) in_ids[j] = j;
+      for (int r = 0; r < R; ++r) out_ids[r] = k + r;
+      rc = run_direct(e, ptr, C, in_ids, out_ids, cells, kernel_kind(p->method, p->w));
+    }
+  } else {
+    DecodeEntry *ent = nullptr;
+    const void *cells = nullptr;
+    rc = decode_entry(e, ids, &ent, &cells);
+    if (rc == 0) rc = run_direct(e, ptr, C, ent->dp.survivors, ent->dp.erased, cells, decode_kind(e, ent));
+  }
+  if (rc == 0) {
+    static std::atomic<bool> warned{false};
+    if (!warned.exchange(true))
+      fprintf(stderr, "lstore_ec: a stripe call failed (%s); retried with direct copies\n", first.c_str());
+    return 0;
+  }
+  tl_err = first + "; direct retry: " + tl_err;
+  return -1;
+}
+
 void fp_encode_block(lio_erasure_plan_t *p, char **ptr, int block_size) {
   PlanExt *e = ext_of(p);
   if (!e) {
     fprintf(stderr, "lstore_ec: encode_block on a plan not created by this library\n");
     abort();
   }
-  if (encode_stripes_impl(e, ptr, 1, block_size) != 0) {
-    fprintf(stderr, "lstore_ec: encode_block failed: %s\n", tl_err.c_str());
-    abort();
-  }
+  if (encode_stripes_impl(e, ptr, 1, block_size) == 0) return;
+  // encode_block cannot report a status, and writing no (or stale) parity would be stamped with
+  // a matching stripe magic by the caller (segment/jerasure.c:1850): retry once, then abort as
+  // Jerasure exits on errors (jerasure.c:306-310)
+  if (retry_direct(e, ptr, block_size, {}) == 0) return;
+  fprintf(stderr, "lstore_ec: encode_block failed: %s\n", tl_err.c_str());
+  abort();
 }
 
 int fp_decode_block(lio_erasure_plan_t *p, char **ptr, int block_size, int *erasures) {
   PlanExt *e = ext_of(p);
   if (!e) return fail("not an lstore_ec plan");
-  return decode_stripes_impl(e, ptr, 1, block_size, erasures);
+  if (decode_stripes_impl(e, ptr, 1, block_size, erasures) == 0) return 0;
+  std::vector<int> ids;
+  if (parse_erasures(p, erasures, ids) != 0) return -1;
+  if (p->method == RAID4 && ids[0] >= p->data_strips) return 0;
+  return retry_direct(e, ptr, block_size, ids);
 }
 
 int fp_dummy(lio_erasure_plan_t *) { return 0; }
@@ -1850,6 +1977,16 @@ int fp_dummy(lio_erasure_plan_t *) { return 0; }
 }  // namespace
 
 namespace lsec {
+
+int set_error(const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  tl_err = buf;
+  return -1;
+}
 
 void parallel_copy(std::vector<HostCopy> &jobs) {
   std::vector<CopyJob> j;
@@ -2240,9 +2377,33 @@ lio_erasure_plan_t *et_generate_plan(long long int file_size, int method, int da
       best_excess = excess;
       best_packet = ps;
       best_size = size;
-      const float pct = (1.0f * excess) / file_size * 100;
-      if (pct < 1) break;
+      // `float increase = (1.0*j) / file_size * 100`: double arithmetic, then stored to a
+      // float, which is what the < 1 test sees (erasure_tools.c:741, :893-894)
+      const float increase = static_cast<float>((1.0 * excess) / file_size * 100);
+      if (increase < 1) break;
     }
+  }
+  // Refused at plan time instead of failing on every block later (the segment maps a NULL plan
+  // to -7 at exnode load, segment/jerasure.c:2237-2240):
+  //  * packet codes asked for k equal chunks (file_size = k*C, what the segment passes,
+  //    :2236) whose C is not a multiple of w * packet_size: the reference builds them, and its
+  //    schedule encode then runs past the chunks (jerasure.c:1193-1207 walks strip_size > C
+  //    bytes).  A file_size that is not k equal chunks is a file-tool request (et_encode pads
+  //    the last strip to strip_size, erasure_tools.c:339-436) and keeps its padded plan.
+  //  * plans no GPU kernel serves (there is no CPU path)
+  const int kind = kernel_kind(method, w);
+  if (kind == KNONE) {
+    fail("et_generate_plan: %s at w=%d has no GPU kernel in this build", JE_method[method], w);
+    return nullptr;
+  }
+  if (data_strips < 1 || data_strips > lsec::kMaxK || parity_strips < 1 || parity_strips > kMaxM) {
+    fail("et_generate_plan: k=%d m=%d outside the engine's 1..%d x 1..%d", data_strips, parity_strips, lsec::kMaxK, kMaxM);
+    return nullptr;
+  }
+  if (packet_kind(kind) && best_size != file_size && file_size % data_strips == 0) {
+    fail("et_generate_plan: %s chunk %lld is not a multiple of w*packet_size = %d (the search padded %lld to %lld)",
+         JE_method[method], file_size / data_strips, w * best_packet, file_size, best_size);
+    return nullptr;
   }
   return et_new_plan(method, best_size / data_strips, data_strips, parity_strips, w, best_packet, base_unit);
 }

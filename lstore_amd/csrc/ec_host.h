@@ -6,6 +6,9 @@
 
 namespace lsec {
 
+// Record a printf-style message for lsec_last_error() (thread-local) and return -1.
+int set_error(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+
 struct HostCopy {
   char *dst;
   const char *src;

@@ -22,8 +22,14 @@ extern "C" {
 
 int lsec_segment_write(lio_erasure_plan_t *plan, const char *data, int nstripes, int chunk, int n_shift,
                        long long first_stripe, char **dev) {
-  if (!plan || !data || !dev || nstripes < 0 || chunk <= 0 || n_shift < 0 || first_stripe < 0) return -1;
+  if (!plan || !data || !dev) return lsec::set_error("lsec_segment_write: plan, data or dev is NULL");
+  if (nstripes < 0 || chunk <= 0 || n_shift < 0 || first_stripe < 0)
+    return lsec::set_error("lsec_segment_write: bad geometry (nstripes=%d chunk=%d n_shift=%d first_stripe=%lld)", nstripes,
+                           chunk, n_shift, first_stripe);
   const int k = plan->data_strips, m = plan->parity_strips, n = k + m;
+  if (k < 1 || m < 1 || n > LSEC_MAX_DEVS) return lsec::set_error("lsec_segment_write: k+m=%d outside 2..%d", n, LSEC_MAX_DEVS);
+  for (int i = 0; i < n; ++i)
+    if (!dev[i]) return lsec::set_error("lsec_segment_write: dev[%d] is NULL", i);
   const size_t C = static_cast<size_t>(chunk), lchunk = C + 4;
   if (nstripes == 0) return 0;
   // ptr[] as segjerase_write_func builds it; parity slots point straight into the images

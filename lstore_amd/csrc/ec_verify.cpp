@@ -226,20 +226,27 @@ int control_check(lio_erasure_plan_t *plan, Stage &S, int w0, int cnt, const std
       else break;                               // m devices bad: nothing can be checked
       continue;
     }
-    lsec::DiffArgs da;
-    std::memset(&da, 0, sizeof(da));
-    da.npairs = static_cast<int>(ctl.size());
-    da.nstripes = cnt;
-    da.size = S.C;
-    da.flags = S.dflag + w0;
-    for (size_t p = 0; p < ctl.size(); ++p) {
-      da.a[p] = {reinterpret_cast<uint64_t>(S.slot(w0, out.slot_of[ctl[p]])), static_cast<int64_t>(m * S.C)};
-      da.b[p] = {reinterpret_cast<uint64_t>(S.chunk(w0, ctl[p])), static_cast<int64_t>(n * S.C)};
+    // up to m - |bad| control chunks: compared in launches of at most kMaxR pairs (the kernel
+    // only sets flags, so the launches OR into one flag per stripe)
+    if (hipMemsetAsync(S.dflag + w0, 0, sizeof(int) * cnt, S.st) != hipSuccess)
+      return lsec::set_error("control check: hipMemsetAsync failed");
+    for (size_t p0 = 0; p0 < ctl.size(); p0 += lsec::kMaxR) {
+      lsec::DiffArgs da;
+      std::memset(&da, 0, sizeof(da));
+      da.npairs = static_cast<int>(std::min<size_t>(lsec::kMaxR, ctl.size() - p0));
+      da.nstripes = cnt;
+      da.size = S.C;
+      da.flags = S.dflag + w0;
+      for (int p = 0; p < da.npairs; ++p) {
+        const int c = ctl[p0 + p];
+        da.a[p] = {reinterpret_cast<uint64_t>(S.slot(w0, out.slot_of[c])), static_cast<int64_t>(m * S.C)};
+        da.b[p] = {reinterpret_cast<uint64_t>(S.chunk(w0, c)), static_cast<int64_t>(n * S.C)};
+      }
+      if (lsec::launch_chunk_diff(da, S.st) != hipSuccess) return lsec::set_error("control check: chunk compare launch failed");
     }
-    if (hipMemsetAsync(S.dflag + w0, 0, sizeof(int) * cnt, S.st) != hipSuccess || lsec::launch_chunk_diff(da, S.st) != hipSuccess ||
-        hipMemcpyAsync(&S.hflag[w0], S.dflag + w0, sizeof(int) * cnt, hipMemcpyDeviceToHost, S.st) != hipSuccess ||
+    if (hipMemcpyAsync(&S.hflag[w0], S.dflag + w0, sizeof(int) * cnt, hipMemcpyDeviceToHost, S.st) != hipSuccess ||
         hipStreamSynchronize(S.st) != hipSuccess)
-      return -1;
+      return lsec::set_error("control check: flag copy failed");
     for (int t = 0; t < cnt; ++t)
       if (S.hflag[w0 + t] && out.pass[t]) {
         out.pass[t] = 0;
@@ -551,8 +558,12 @@ extern "C" {
 // ============================================================================ read
 int lsec_segment_read(lio_erasure_plan_t *plan, char **dev, int nstripes, int chunk, int n_shift, long long first_stripe,
                       int flags, char *data_out, int *status) {
-  if (!plan || !dev || !data_out || nstripes < 0 || chunk <= 0 || chunk % 8 != 0 || n_shift < 0 || first_stripe < 0) return -1;
+  if (!plan || !dev || !data_out) return lsec::set_error("lsec_segment_read: plan, dev or data_out is NULL");
+  if (nstripes < 0 || chunk <= 0 || chunk % 8 != 0 || n_shift < 0 || first_stripe < 0)
+    return lsec::set_error("lsec_segment_read: bad geometry (nstripes=%d chunk=%d n_shift=%d first_stripe=%lld)", nstripes,
+                           chunk, n_shift, first_stripe);
   const int k = plan->data_strips, m = plan->parity_strips, n = k + m;
+  if (k < 1 || m < 1 || n > LSEC_MAX_DEVS) return lsec::set_error("lsec_segment_read: k+m=%d outside 2..%d", n, LSEC_MAX_DEVS);
   const size_t C = static_cast<size_t>(chunk), lchunk = C + 4;
   const bool paranoid = flags & LSEC_READ_PARANOID, cksum = !(flags & LSEC_MAGIC_LEGACY);
   if (nstripes == 0) return 0;
@@ -607,7 +618,8 @@ int lsec_segment_read(lio_erasure_plan_t *plan, char **dev, int nstripes, int ch
   std::vector<Repair> repair(nstripes);
   hipStream_t stream = nullptr;
   if (!work.empty()) keep_pool();
-  if (!work.empty() && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return -1;
+  if (!work.empty() && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess)
+    return lsec::set_error("lsec_segment_read: cannot create a HIP stream");
   tr.st = stream;
   BruteState bs;
   int rc = 0;
@@ -615,7 +627,10 @@ int lsec_segment_read(lio_erasure_plan_t *plan, char **dev, int nstripes, int ch
   for (size_t b0 = 0; b0 < work.size() && rc == 0; b0 += wmax) {
     const int W = static_cast<int>(std::min<size_t>(wmax, work.size() - b0));
     Stage S;
-    if (S.alloc(W, n, m, C, stream) != 0) { rc = -1; break; }
+    if (S.alloc(W, n, m, C, stream) != 0) {
+      rc = lsec::set_error("lsec_segment_read: cannot allocate a %d-stripe stage in HBM", W);
+      break;
+    }
     std::vector<std::vector<int>> bad(W);
     std::vector<Magic> mg(W);
     std::vector<lsec::DevPiece> pieces;  // chunks in staging order; unreadable devices stage zeros
@@ -677,9 +692,11 @@ int lsec_segment_read(lio_erasure_plan_t *plan, char **dev, int nstripes, int ch
 // ============================================================================ inspect
 int lsec_segment_inspect(lio_erasure_plan_t *plan, char *buf, int nstripes, int chunk, int flags, int *stripe_status,
                          unsigned char *badmap, unsigned char *rewrite, lsec_inspect_state_t *state) {
-  if (!plan || !buf || !state || nstripes < 0 || chunk <= 0 || chunk % 8 != 0) return -1;
+  if (!plan || !buf || !state) return lsec::set_error("lsec_segment_inspect: plan, buf or state is NULL");
+  if (nstripes < 0 || chunk <= 0 || chunk % 8 != 0)
+    return lsec::set_error("lsec_segment_inspect: bad geometry (nstripes=%d chunk=%d)", nstripes, chunk);
   const int k = plan->data_strips, m = plan->parity_strips, n = k + m;
-  if (n > LSEC_MAX_DEVS) return -1;
+  if (k < 1 || m < 1 || n > LSEC_MAX_DEVS) return lsec::set_error("lsec_segment_inspect: k+m=%d outside 2..%d", n, LSEC_MAX_DEVS);
   const size_t C = static_cast<size_t>(chunk), lchunk = C + 4;
   const bool do_fix = flags & LSEC_INSPECT_FIX, cksum = !(flags & LSEC_MAGIC_LEGACY);
   if (nstripes == 0) return 0;
@@ -721,13 +738,17 @@ int lsec_segment_inspect(lio_erasure_plan_t *plan, char *buf, int nstripes, int 
   for (int s = 0; s < nstripes; ++s) final_bad[s] = q[s].bad;
   hipStream_t stream = nullptr;
   if (!work.empty()) keep_pool();
-  if (!work.empty() && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return -1;
+  if (!work.empty() && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess)
+    return lsec::set_error("lsec_segment_inspect: cannot create a HIP stream");
   const int wmax = stripes_per_batch(n, m, C);
   int rc = 0;
   for (size_t b0 = 0; b0 < work.size() && rc == 0; b0 += wmax) {
     const int W = static_cast<int>(std::min<size_t>(wmax, work.size() - b0));
     Stage S;
-    if (S.alloc(W, n, m, C, stream) != 0) { rc = -1; break; }
+    if (S.alloc(W, n, m, C, stream) != 0) {
+      rc = lsec::set_error("lsec_segment_inspect: cannot allocate a %d-stripe stage in HBM", W);
+      break;
+    }
     // stage the chunks ([magic | chunk] records -> chunks), packed into large DMAs
     std::vector<lsec::DevPiece> pieces;
     pieces.reserve(static_cast<size_t>(W) * n);

@@ -313,7 +313,7 @@ int eco_generate_plan(long long file_size, int method, int k, int m, int w, int 
         int excess = (int)(sz - file_size);          /* int as in the reference */
         if (excess <= best_excess) {
             best_excess = excess; best_p = p; best_size = sz;
-            float pct = (1.0f * excess) / file_size * 100;
+            float pct = (float)((1.0 * excess) / file_size * 100);  /* double, stored to float (:893-894) */
             if (pct < 1) break;
         }
     }

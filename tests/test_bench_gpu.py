@@ -1,0 +1,36 @@
+"""bench.py's own multi-rank path on the GPU box: `bench.py --gpus 2` with no external launcher
+(two ranks spawned by bench.py itself, sharing the one GPU over gloo), checked for the JSON
+contract.  8-GPU runs belong to the driver; this is the N > 1 code path at small size."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+def test_bench_self_launches_two_ranks(cuda, tmp_path):
+    out = tmp_path / "line.json"
+    env = dict(os.environ, LSEC_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "2", "--stripes", "64", "--steps", "3", "--warmup", "1",
+                        "--no-cpu", "--no-host-path", "--json-out", str(out)],
+                       cwd=ROOT, env=env, timeout=240, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = json.loads(out.read_text())
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert [p["rank"] for p in line["per_rank"]] == [0, 1]
+    assert all(p["parity_ok"] and p["stripes"] == 64 for p in line["per_rank"])
+    assert line["parity_check"].startswith("bit-exact")
+    assert line["value"] > 0 and line["roofline"]["frac"] > 0
+
+
+def test_bench_refuses_mismatched_world_size(tmp_path):
+    """(CPU) under an external launcher, WORLD_SIZE must equal --gpus"""
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--stripes", "8"], cwd=ROOT, env=env, timeout=120,
+                       capture_output=True, text=True)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stdout

@@ -1,72 +1,149 @@
-"""world_size-2 gloo rehearsal of the multi-GPU path (CPU only).
+"""world_size-2 gloo rehearsal of bench.py's multi-GPU path (CPU only).
 
-bench.py shards stripes statically over ranks with no data-path collective; these tests run
-the same partition + timing reductions on two CPU processes and check that the union of the
-per-rank work equals the single-process result (oracle encode of every stripe).
+The ranks run bench.py's own code: ``bench.launch`` self-spawns them (WORLD_SIZE unset,
+``--gpus 2``) and each runs ``bench.run_rank`` -- partition, warm-up, the barrier-bracketed
+timed region, max-over-ranks, per-rank gather and rank 0's JSON line.  Only the engine is
+swapped: ``OracleEngine`` below stands in for ``bench.HipEngine`` (no GPU here) and encodes /
+decodes with the CPU restatement, recording a CRC per global stripe so the test can check that
+the union of the ranks' work is exactly the single-process result.
 """
+import json
 import os
-import socket
+import time
 import zlib
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
 
+import bench
 from lstore_amd.partition import stripe_range
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+class OracleEngine:
+    """bench.HipEngine's interface over the CPU oracle (test infrastructure only)."""
+
+    def __init__(self, a, rank, world, local):
+        import oracle as O
+
+        self.O, self.a, self.rank = O, a, rank
+        self.method = O.REED_SOL_VAN if a.method == "reed_sol_van" else O.CAUCHY_GOOD
+        self.P = O.generate_plan(a.k * a.chunk, self.method, a.k, a.m)["packet_size"]
+        self.kernel = 1
+        self.stripes = None
+
+    def init_dist(self, dist):
+        dist.init_process_group("gloo")
+
+    def reduce_device(self, dist):
+        return None
+
+    def workload(self, N, pad, seed, first=0):
+        from patterns import stripe
+
+        a, O = self.a, self.O
+        self.first = first
+        self.stripes = np.zeros((N, a.k + a.m, a.chunk), np.uint8)
+        for s in range(N):
+            self.stripes[s, :a.k] = stripe(a.k, a.chunk, first + s)
+        self.rebuilt = np.zeros((N, a.chunk), np.uint8)
+
+        def encode():
+            for s in range(N):
+                self.stripes[s, a.k:] = O.encode(self.method, self.stripes[s, :a.k], a.m, self.P)
+
+        def decode():
+            for s in range(N):
+                sh = self.stripes[s].copy()
+                sh[a.lost] = 0
+                assert O.decode(self.method, sh, a.k, [a.lost], self.P) == 0
+                self.rebuilt[s] = sh[a.lost]
+
+        return encode, decode
+
+    def sync(self):
+        pass
+
+    def launch_times(self, encode, decode, reps):
+        t0 = time.perf_counter()
+        encode()
+        t1 = time.perf_counter()
+        decode()
+        return max(t1 - t0, 1e-9), max(time.perf_counter() - t1, 1e-9)
+
+    def check(self, N):
+        ok = all(np.array_equal(self.rebuilt[s], self.stripes[s, self.a.lost]) for s in range(N))
+        dump = os.environ.get("LSEC_TEST_DUMP")
+        if dump:
+            crcs = {self.first + s: zlib.crc32(self.stripes[s, self.a.k:].tobytes()) for s in range(N)}
+            with open(os.path.join(dump, f"rank{self.rank}.json"), "w") as f:
+                json.dump(crcs, f)
+        return ok, "rebuilt == lost shard (oracle engine)"
+
+    def extras(self, N, t_enc, t_dec, rank, world):
+        return {}
+
+    def kernel_name(self):
+        return "oracle (test engine)"
+
+    def traffic(self, N):
+        return None, None
+
+    def close(self):
+        self.stripes = None
 
 
-def _worker(rank, world, port, nstripes, out_q):
-    import torch.distributed as dist
+def _args(*extra):
+    return bench.parse(["--chunk", "4096", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-host-path",
+                        "--no-layout-ab", "--no-copy-ref", *extra])
 
+
+@pytest.mark.parametrize("total", [7, 16])
+def test_self_launched_two_ranks_match_single_process(built, tmp_path, monkeypatch, total):
+    """bench.launch(--gpus 2) with no external launcher: two gloo ranks, strong partition."""
     import oracle as O
-    from lstore_amd.partition import max_over_ranks, stripe_range, sum_over_ranks
     from patterns import stripe
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    s0, s1 = stripe_range(nstripes, world, rank)
-    crcs = {}
-    for s in range(s0, s1):
-        par = O.encode(O.REED_SOL_VAN, stripe(6, 4096, s), 3)
-        crcs[s] = zlib.crc32(par.tobytes())
-    dist.barrier()
-    slowest = max_over_ranks(float(rank + 1))
-    total = sum_over_ranks(s1 - s0)
-    out_q.put((rank, crcs, slowest, total))
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("nstripes", [7, 16])
-def test_two_rank_partition_matches_single_process(built, nstripes):
-    import oracle as O
-    from patterns import stripe
-
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, nstripes, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=120) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setenv("LSEC_TEST_DUMP", str(tmp_path))
+    out = tmp_path / "line.json"
+    rc = bench.launch(_args("--gpus", "2", "--total-stripes", str(total), "--json-out", str(out)), OracleEngine)
+    assert rc == 0
+    line = json.loads(out.read_text())
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert [r["rank"] for r in line["per_rank"]] == [0, 1]
+    assert [r["stripes"] for r in line["per_rank"]] == [b - a for a, b in (stripe_range(total, 2, r) for r in range(2))]
+    assert all(r["parity_ok"] for r in line["per_rank"])
+    assert line["value"] > 0 and line["ms_per_step"] > 0
     merged = {}
-    for rank, crcs, slowest, total in res:
-        assert slowest == 2.0 and total == nstripes
-        assert not set(crcs) & set(merged)
-        merged.update(crcs)
-    assert sorted(merged) == list(range(nstripes))
-    for s in range(nstripes):
+    for r in range(2):
+        part = {int(s): c for s, c in json.loads((tmp_path / f"rank{r}.json").read_text()).items()}
+        assert not set(part) & set(merged)
+        merged.update(part)
+    assert sorted(merged) == list(range(total))
+    for s in range(total):
         assert merged[s] == zlib.crc32(O.encode(O.REED_SOL_VAN, stripe(6, 4096, s), 3).tobytes())
+
+
+def test_self_launched_weak_scaling(built, tmp_path, monkeypatch):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setenv("LSEC_TEST_DUMP", str(tmp_path))
+    out = tmp_path / "line.json"
+    rc = bench.launch(_args("--gpus", "2", "--stripes", "3", "--method", "cauchy_good", "--json-out", str(out)),
+                      OracleEngine)
+    assert rc == 0
+    line = json.loads(out.read_text())
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert [r["stripes"] for r in line["per_rank"]] == [3, 3]
+    seen = set()
+    for r in range(2):
+        seen |= {int(s) for s in json.loads((tmp_path / f"rank{r}.json").read_text())}
+    assert seen == set(range(6))  # rank r owns stripes [3r, 3r+3)
+
+
+def test_world_size_must_match_gpus(built, monkeypatch, capsys):
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert bench.launch(_args("--gpus", "4"), OracleEngine) == 2
+    assert "WORLD_SIZE=2" in capsys.readouterr().out
 
 
 def test_stripe_range_properties():
@@ -80,3 +157,10 @@ def test_stripe_range_properties():
     with pytest.raises(ValueError):
         stripe_range(10, 2, 2)
     assert np.sum([b - a for a, b in (stripe_range(10, 3, r) for r in range(3))]) == 10
+
+
+def test_usable_cpus_reports_quota_and_visible():
+    threads, visible, quota = bench.usable_cpus()
+    assert 1 <= threads <= visible
+    if quota:
+        assert threads <= quota

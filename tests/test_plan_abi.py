@@ -96,14 +96,30 @@ def test_plans_match_reference_fixtures(built, golden):
 
 
 def test_form_decoding_before_encoding_quirk(built):
-    # cauchy_*_form_coding_matrix returns -1 while no schedule exists (erasure_tools.c:142/:159)
-    with L.Plan.new(L.CAUCHY_GOOD, 0, 6, 3, 8, 8, 8) as p:
+    # cauchy_*_form_coding_matrix returns -1 when it forms the matrix while no schedule exists
+    # (erasure_tools.c:142/:159), and 0 on every later call ("Already formed", :137/:152)
+    for method in (L.CAUCHY_GOOD, L.CAUCHY_ORIG):
+        with L.Plan.new(method, 0, 6, 3, 8, 8, 8) as p:
+            assert p.form_decoding_matrix() == -1
+            assert p.matrix() is not None and p.bitmatrix() is not None and p.schedule() is None
+            assert p.form_decoding_matrix() == 0
+            assert p.form_decoding_matrix() == 0
+            assert p.form_encoding_matrix() == 0  # early return in the reference; we also fill the schedule
+            assert p.form_decoding_matrix() == 0
+    # liberation family: the same on the bitmatrix (:169-204)
+    with L.Plan.new(L.LIBERATION, 0, 5, 2, 5, 8, 8) as p:
         assert p.form_decoding_matrix() == -1
-        assert p.matrix() is not None and p.bitmatrix() is not None and p.schedule() is None
-        assert p.form_encoding_matrix() == 0  # early return in the reference; we also fill the schedule
+        assert p.form_decoding_matrix() == 0
     with L.Plan.new(L.REED_SOL_VAN, 0, 6, 3, 8, 8, 8) as p:
         assert p.form_decoding_matrix() == 0
+        assert p.form_decoding_matrix() == 0
         assert p.bitmatrix() is None and p.schedule() is None
+
+
+def test_form_decoding_after_encoding(built):
+    with L.Plan.new(L.CAUCHY_GOOD, 0, 6, 3, 8, 8, 8) as p:
+        assert p.form_encoding_matrix() == 0 and p.schedule() is not None
+        assert p.form_decoding_matrix() == 0
 
 
 @pytest.mark.parametrize("method", [L.REED_SOL_VAN, L.CAUCHY_GOOD, L.CAUCHY_ORIG, L.REED_SOL_R6_OP, L.RAID4,
@@ -112,11 +128,41 @@ def test_generate_plan_matches_restatement(built, method):
     k, m = (6, 2) if method in (L.REED_SOL_R6_OP, L.LIBERATION, L.BLAUM_ROTH, L.LIBER8TION) else (6, 3)
     if method == L.RAID4:
         m = 1
+    packet_code = method in (L.CAUCHY_GOOD, L.CAUCHY_ORIG, L.LIBERATION, L.BLAUM_ROTH, L.LIBER8TION)
     for fsize in [k * 16384, k * 65536, k * 262144, k * 1048576, k * 196608, k * 100000, 12345678, 1000, 6 * 4096]:
         ref = O.generate_plan(fsize, method, k, m)
+        if packet_code and ref["strip_size"] * k != fsize and fsize % k == 0:
+            # k chunks of C = fsize / k that no packet size divides: the reference builds this
+            # plan and its schedule encode then overruns the chunks; the engine refuses it at
+            # plan time (the segment maps NULL to -7).  Sizes that are not k equal chunks are
+            # file-tool requests and keep the reference's padded plan.
+            with pytest.raises(E.ErasureError, match="not a multiple of w\\*packet_size"):
+                L.Plan.generate(fsize, method, k, m)
+            continue
         with L.Plan.generate(fsize, method, k, m) as p:
             assert (p.w, p.packet_size, p.strip_size, p.base_unit) == (
                 ref["w"], ref["packet_size"], ref["strip_size"], ref["base_unit"]), (method, fsize)
+
+
+def test_generate_plan_increase_is_double_then_float(built):
+    # `increase = (1.0*j) / file_size * 100` is computed in double and stored to a float
+    # (erasure_tools.c:741, :893-894).  At this size the search stops at P = 4032 that way; the
+    # same expression in float arithmetic gives 1.0 there and goes on to 4024.
+    fsize = 18395501
+    ref = O.generate_plan(fsize, L.REED_SOL_VAN, 6, 3)
+    assert ref["packet_size"] == 4032
+    with L.Plan.generate(fsize, L.REED_SOL_VAN, 6, 3) as p:
+        assert (p.packet_size, p.strip_size) == (4032, ref["strip_size"])
+    excess = ref["strip_size"] * 6 - fsize
+    assert np.float32((1.0 * excess) / fsize * 100) < 1
+    assert np.float32(excess) / np.float32(fsize) * np.float32(100) >= 1
+
+
+def test_generate_plan_refuses_what_no_kernel_serves(built):
+    with pytest.raises(E.ErasureError, match="not a multiple"):
+        L.Plan.generate(6 * 100000, L.CAUCHY_GOOD, 6, 3)   # strip 100352, P = 784: C = 100000 cannot be encoded
+    with L.Plan.generate(6 * 100000, L.REED_SOL_VAN, 6, 3) as p:  # matrix codes take any C % 8 == 0
+        assert p.kernel == 1
 
 
 def test_generate_plan_rejects_what_the_reference_rejects(built):

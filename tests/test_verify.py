@@ -169,3 +169,39 @@ def test_read_matches_reference(cuda, method, k, m, C, legacy, paranoid):
         assert st[s] == rst[s], (s, kinds[s], st[s], rst[s])
         if st[s] >= 0:
             assert np.array_equal(out[s], rout[s]), (s, kinds[s])
+
+
+@pytest.mark.gpu
+@needs_ref
+@pytest.mark.parametrize("fix", [False, True])
+def test_legacy_inspect_with_more_controls_than_one_compare_launch(cuda, fix):
+    """Legacy magics with m = 18: up to m - |bad| = 17-18 control chunks per window, more than one
+    chunk-compare launch holds (kMaxR = 16 pairs), so the comparison runs in several launches
+    OR-ing into one flag per stripe.  Damage is limited to stale magics and single silent
+    corruptions (the brute-force search over C(22, <= 17) sets would not finish for worse)."""
+    method, k, m, C, nstr = L.REED_SOL_VAN, 4, 18, 1024, 12
+    n = k + m
+    data = np.stack([stripe(k, C, s + 77) for s in range(nstr)])
+    with L.Plan.for_chunk(method, k, m, C) as p:
+        img = p.segment_write(data, 1, 0)
+    buf = logical_records(img, nstr, C, n)
+    rng = np.random.default_rng(18)
+    for s in range(nstr):
+        buf[s, :, :4] = rng.integers(1, 255, 4, dtype=np.uint8)   # legacy: one arbitrary magic per stripe
+        if s % 3 == 1:
+            buf[s, int(rng.integers(0, n)), 0] ^= 0x11              # stale magic on one device
+        elif s % 3 == 2:
+            buf[s, int(rng.integers(0, n)), 4 + int(rng.integers(0, C))] ^= 0x5A  # silent corruption
+    with L.Plan.for_chunk(method, k, m, C) as p:
+        ours = buf.copy()
+        st, bm, rw, state = p.segment_inspect(ours, C, fix=fix, legacy_magic=True)
+        rp = O.RefPlan(method, k, m, 8, p.packet_size)
+        ref = buf.copy()
+        rst, rbm, rrw, cnt, brute = rp.segment_inspect(ref, nstr, C, 0, int(fix))
+    assert st.tolist() == rst.tolist()
+    assert np.array_equal(bm, rbm) and np.array_equal(rw, rrw)
+    assert [state.bad_stripes, state.unrecoverable, state.silent_errors, state.empty_stripes] == cnt.tolist()
+    assert 3 in st.tolist()   # the silent corruptions were found by the (short) brute-force search
+    if fix:
+        sel = rw.astype(bool)
+        assert np.array_equal(ours[sel], ref[sel])

@@ -46,7 +46,7 @@ def annotate(res, extra):
     def arg(name, default):
         return int(extra[extra.index(name) + 1]) if name in extra else default
     k, m, C, N = arg("--k", 6), arg("--m", 3), arg("--chunk", 1 << 20), arg("--stripes", 4096)
-    res.update({"bench_stripes": N, "chunk": C, "k": k, "m": m})
+    res.update({"bench_stripes": N, "chunk": C, "k": k, "m": m, "pad": arg("--pad", 0)})
     for name, v in res["kernels"].items():
         if "k_hbm_copy" in name:  # bench.py's ceiling probe: (k+m)*C*N/2 bytes read and written
             v["algorithmic"] = (k + m) * C * N
@@ -60,7 +60,7 @@ def annotate(res, extra):
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     extra = sys.argv[2:]
-    bench_args = ["--steps", "2", "--warmup", "1", "--no-cpu", "--no-host-path"] + extra
+    bench_args = ["--steps", "2", "--warmup", "1", "--no-cpu", "--no-host-path", "--no-layout-ab", "--no-copy-ref"] + extra
     out = os.path.join(ROOT, "gpurun_out", f"pmc_{tag}")
     fetch = run_pass("FETCH_SIZE", os.path.join(out, "fetch"), bench_args)
     write = run_pass("WRITE_SIZE", os.path.join(out, "write"), bench_args)
