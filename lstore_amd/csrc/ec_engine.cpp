@@ -1342,15 +1342,22 @@ int device_layout(const lio_erasure_plan_t *p, char **ptrs, int nstripes, std::v
 }
 
 hipStream_t thread_stream() {
-  // per-thread blocking stream for the synchronous fn-pointer entry points
-  static thread_local std::map<int, hipStream_t> streams;
+  // per-thread stream for the synchronous fn-pointer entry points, destroyed when the thread
+  // exits (a caller that churns threads does not accumulate streams)
+  struct Streams {
+    std::map<int, hipStream_t> by_dev;
+    ~Streams() {
+      for (auto &kv : by_dev) (void)hipStreamDestroy(kv.second);
+    }
+  };
+  static thread_local Streams streams;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  auto it = streams.find(dev);
-  if (it != streams.end()) return it->second;
+  auto it = streams.by_dev.find(dev);
+  if (it != streams.by_dev.end()) return it->second;
   hipStream_t s = nullptr;
   if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-  streams[dev] = s;
+  streams.by_dev[dev] = s;
   return s;
 }
 
@@ -1676,11 +1683,154 @@ int run_coalesced(PlanExt *e, char **ptrs, int nstripes, long long C, const std:
   return Dispatcher::for_device(dev)->run(r);
 }
 
-// host-memory batches: small ones are coalesced with concurrent callers, large ones stream
-// through their own staging pipeline
+// ---------------------------------------------------------------- zero-copy small calls
+// LStore calls encode_block / decode_block once per stripe (16 KiB chunks by default,
+// cjerase_16k.ex3:46) from many pool threads.  For such calls the DMA round trip (H2D, kernel,
+// D2H, each a queue operation with its own fixed cost, plus the hops through a dispatcher
+// thread) dominates: 78 us per 16 KiB Cauchy(6+3) call at one thread in round 1.  Here the
+// calling thread copies its chunks into its own page-locked slot and the coding kernel reads
+// and writes that slot over PCIe directly (zero-copy): one launch on the thread's stream and
+// one synchronisation per call, no DMA and no other thread.  Chunks the caller already holds
+// in page-locked memory are read and written in place, with no copies at all.
+size_t zerocopy_limit() {  // per-call bytes (inputs + outputs) served this way; LSEC_ZEROCOPY_KB
+  static size_t b = [] {
+    const char *s = getenv("LSEC_ZEROCOPY_KB");
+    return static_cast<size_t>(std::max(0L, s ? atol(s) : 1024L)) << 10;
+  }();
+  return b;
+}
+
+struct ZcSlot {  // one calling thread's page-locked slot on one device
+  char *h = nullptr;
+  uint64_t d = 0;  // its device address
+  size_t cap = 0;
+  // completion: flag in coherent page-locked memory (the host spins on it), the signal
+  // kernel's arrival counter in device memory, and the value the next call waits for
+  unsigned *flag = nullptr, *dflag = nullptr, *counter = nullptr;
+  unsigned seq = 0;
+  ZcSlot() = default;
+  ZcSlot(const ZcSlot &) = delete;
+  ZcSlot &operator=(const ZcSlot &) = delete;
+  ~ZcSlot() {
+    if (h) (void)hipHostFree(h);
+    if (flag) (void)hipHostFree(flag);
+    if (counter) (void)hipFree(counter);
+  }
+  int init_signal() {
+    if (flag) return 0;
+    HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&flag), 64, hipHostMallocCoherent));
+    *flag = 0;
+    void *d = nullptr;
+    HIP_OK(hipHostGetDevicePointer(&d, flag, 0));
+    dflag = static_cast<unsigned *>(d);
+    HIP_OK(hipMalloc(reinterpret_cast<void **>(&counter), 64));
+    HIP_OK(hipMemset(counter, 0, 64));
+    return 0;
+  }
+};
+
+// Completes a zero-copy call: the signal kernel behind the coding kernel on `st`, then a spin
+// on the flag (a flag seen ~8 us sooner than hipStreamSynchronize returns:
+// tools/probes/zc_probe.hip, profiles/r02_v3_zc_probe.txt).  A call whose flag has not come
+// after a second falls back to the stream's own status, so a failed launch is reported.
+int zc_complete(ZcSlot &sl, hipStream_t st) {
+  const unsigned v = ++sl.seq == 0 ? ++sl.seq : sl.seq;
+  const hipError_t e = lsec::launch_signal(sl.counter, sl.dflag, v, st);
+  if (e != hipSuccess) return fail("signal launch: %s", hipGetErrorString(e));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spins = 0; __atomic_load_n(sl.flag, __ATOMIC_ACQUIRE) != v; ++spins) {
+    __builtin_ia32_pause();
+    if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+      HIP_OK(hipStreamSynchronize(st));
+      if (__atomic_load_n(sl.flag, __ATOMIC_ACQUIRE) != v) return fail("zero-copy call: completion flag never came");
+      break;
+    }
+  }
+  return 0;
+}
+
+// regular stripe stride of device addresses a[s * per + i] (i < per): shard i of stripe s at
+// a[i] + s * stride[i]; false if irregular
+bool regular_refs(const std::vector<uint64_t> &a, int nstripes, size_t per, std::vector<int64_t> &stride) {
+  stride.assign(per, 0);
+  if (nstripes < 2) return true;
+  for (size_t i = 0; i < per; ++i) stride[i] = static_cast<int64_t>(a[per + i] - a[i]);
+  for (int s = 2; s < nstripes; ++s)
+    for (size_t i = 0; i < per; ++i)
+      if (a[s * per + i] != a[i] + static_cast<uint64_t>(s * stride[i])) return false;
+  return true;
+}
+
+int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
+                 const std::vector<int> &out_ids, const void *image, int kind) {
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  hipStream_t st = thread_stream();
+  if (!st) return fail("no HIP stream");
+  const lio_erasure_plan_t *p = &e->pub;
+  const int km = p->data_strips + p->parity_strips;
+  const size_t nin = in_ids.size(), nout = out_ids.size(), nio = nin + nout;
+  ShardRef in[lsec::kMaxK], out[kMaxM];
+  const bool aligned = kernel_transport_aligned(ptrs, nstripes, km, in_ids, out_ids, C, C);
+  static thread_local std::map<int, std::unique_ptr<ZcSlot>> slots;
+  std::unique_ptr<ZcSlot> &slot = slots[dev];
+  if (!slot) slot.reset(new ZcSlot());
+  if (slot->init_signal()) return -1;
+  CallerPinned cp = caller_pinned(ptrs, nstripes, km, in_ids, out_ids, C, aligned);
+  std::vector<int64_t> stride;
+  if (cp.by_kernel && regular_refs(cp.dev, nstripes, nio, stride)) {
+    // caller page-locked chunks: read and written in place over PCIe
+    for (size_t j = 0; j < nin; ++j) in[j] = {cp.dev[j], stride[j]};
+    for (size_t r = 0; r < nout; ++r) out[r] = {cp.dev[nin + r], stride[nin + r]};
+    if (enqueue_apply(kind, image, static_cast<int>(nin), static_cast<int>(nout), in, out, nstripes, C, p->packet_size, st, p->w))
+      return -1;
+    return zc_complete(*slot, st);
+  }
+  const size_t need = static_cast<size_t>(nstripes) * nio * static_cast<size_t>(C);
+  if (slot->cap < need) {
+    if (slot->h) (void)hipHostFree(slot->h);
+    slot->h = nullptr;
+    slot->cap = 0;
+    const size_t cap = std::max<size_t>(need, 256u << 10);
+    // coherent: the kernel's reads and writes of the slot go straight over PCIe, none stays in an L2
+    HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&slot->h), cap, hipHostMallocCoherent));
+    void *d = nullptr;
+    HIP_OK(hipHostGetDevicePointer(&d, slot->h, 0));
+    slot->d = reinterpret_cast<uint64_t>(d);
+    slot->cap = cap;
+  }
+  // slot layout: inputs [s][nin][C], then outputs [s][nout][C]
+  const size_t in_bytes = static_cast<size_t>(nstripes) * nin * C;
+  for (int s = 0; s < nstripes; ++s)
+    for (size_t j = 0; j < nin; ++j)
+      std::memcpy(slot->h + (s * nin + j) * C, ptrs[static_cast<size_t>(s) * km + in_ids[j]], C);
+  for (size_t j = 0; j < nin; ++j) in[j] = {slot->d + j * C, static_cast<int64_t>(nin * C)};
+  for (size_t r = 0; r < nout; ++r) out[r] = {slot->d + in_bytes + r * C, static_cast<int64_t>(nout * C)};
+  if (enqueue_apply(kind, image, static_cast<int>(nin), static_cast<int>(nout), in, out, nstripes, C, p->packet_size, st, p->w))
+    return -1;
+  if (zc_complete(*slot, st)) return -1;
+  for (int s = 0; s < nstripes; ++s)
+    for (size_t r = 0; r < nout; ++r)
+      std::memcpy(ptrs[static_cast<size_t>(s) * km + out_ids[r]], slot->h + in_bytes + (s * nout + r) * C, C);
+  return 0;
+}
+
+// which route serves a host-memory call (LSEC_SMALL_PATH: zerocopy | dispatch; default
+// zerocopy up to zerocopy_limit(), the dispatcher up to coalesce_limit(), then run_host)
+bool zerocopy_enabled() {
+  static const bool on = [] {
+    const char *s = getenv("LSEC_SMALL_PATH");
+    return !s || strcmp(s, "dispatch") != 0;
+  }();
+  return on;
+}
+
+// host-memory batches: small ones are served zero-copy by the calling thread (or coalesced
+// with concurrent callers), large ones stream through their own staging pipeline
 int run_host_auto(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
                   const std::vector<int> &out_ids, const void *image, int kind) {
   const size_t bytes = static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()) * C;
+  if (zerocopy_enabled() && bytes <= zerocopy_limit()) return run_zerocopy(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
   if (bytes <= coalesce_limit()) return run_coalesced(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
   return run_host(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
 }

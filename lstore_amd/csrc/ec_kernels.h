@@ -119,6 +119,13 @@ struct CopyPiece {
 };
 hipError_t launch_copy_pieces(const CopyPiece *list, int n, hipStream_t stream);
 
+// Completion signal of a zero-copy call: every block writes back its XCD's L2 at system scope
+// (a call's kernel may have left dirty lines of page-locked host memory in any XCD's L2), the
+// last block to arrive (agent-scope counter in device memory, reset by it) stores `value` to
+// `flag` (page-locked host memory) with system-scope release.  Launched on the call's stream
+// right after its coding kernel, so stream order puts every byte the call wrote before the flag.
+hipError_t launch_signal(unsigned *counter, unsigned *flag, unsigned value, hipStream_t stream);
+
 // HBM probe (measurement only): dst <- src, bytes a multiple of 16, both 16-byte aligned.
 hipError_t launch_hbm_copy(void *dst, const void *src, uint64_t bytes, hipStream_t stream);
 

@@ -280,7 +280,28 @@ __global__ __launch_bounds__(kBlock) void k_copy_pieces(const CopyPiece *list, i
   }
 }
 
+// one block per XCD (blocks b, b+8, ... are dealt to one XCD), so the system-scope release
+// fence of each block writes back every XCD's L2
+constexpr int kSignalBlocks = 8;
+__global__ __launch_bounds__(64) void k_signal(unsigned *counter, unsigned *flag, unsigned value) {
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_signal(unsigned *counter, unsigned *flag, unsigned value, hipStream_t st) {
+  if (!counter || !flag) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_signal, dim3(kSignalBlocks), dim3(64), 0, st, counter, flag, value);
+  return hipGetLastError();
+}
 
 hipError_t launch_copy_pieces(const CopyPiece *list, int n, hipStream_t st) {
   if (n <= 0) return hipSuccess;

@@ -1,17 +1,26 @@
 /*
- * tools/fnptr_bench.c -- the unmodified LStore call pattern, in C, against liblstore_ec.so.
+ * tools/fnptr_bench.c -- the unmodified LStore call pattern, in C, against liblstore_ec.so,
+ * with the reference (vendor/jerasure via oracle/_ref) timed the same way beside it.
  *
- * T pthreads share one plan and each calls plan->encode_block(plan, ptr, C) on its own
- * host buffers, one stripe per call, exactly as segjerase_write_func does from the gop pool
- * (src/lio/segment/jerasure.c:1847, :1937).  Prints per-call latency percentiles and the
- * aggregate user-data rate.  Also a compile-time proof that a C caller needs nothing but
- * include/lstore_ec.h and -llstore_ec.
+ * T pthreads share one plan and each calls plan->encode_block(plan, ptr, C) (or
+ * plan->decode_block with data shard 0 lost) on its own host buffers, one stripe per call,
+ * exactly as segjerase_write_func / jerase_control_check do from the gop pool
+ * (src/lio/segment/jerasure.c:1847, :245, :1937).  The threads live for the whole run, like
+ * the pool's: a warm-up phase (per-thread streams, slots, device images, galois tables), then a
+ * timed phase of fixed duration between two barriers.  Runs last long enough (default 2 s) that
+ * a CPU quota enforced per scheduler period (the GPU box grants 16 CPUs of a larger machine)
+ * is what the threads get, not a burst.  Prints per-call latency percentiles and the aggregate
+ * user-data rate as one JSON line per implementation.  Also a compile-time proof that a C
+ * caller needs nothing but include/lstore_ec.h and -llstore_ec.
  *
  * build: gcc -O2 -o build/fnptr_bench tools/fnptr_bench.c -Iinclude -Llstore_amd -llstore_ec \
- *            -Wl,-rpath,'$ORIGIN/../lstore_amd' -lpthread
- * run:   build/fnptr_bench <chunk> <threads> <calls_per_thread> [method]
- *        FNPTR_PINNED=1: each thread's buffer is page-locked (hipHostMalloc, looked up at run
- *        time from libamdhip64.so), as an LStore cache that pins its pages would hold it
+ *            -Wl,-rpath,'$ORIGIN/../lstore_amd' -lpthread -ldl
+ * run:   build/fnptr_bench <chunk> <threads> <seconds> [method] [encode|decode]
+ *        FNPTR_PINNED=1  each thread's buffer is page-locked (hipHostMalloc, looked up at run time
+ *                        from libamdhip64.so), as an LStore cache that pins its pages would hold it
+ *        FNPTR_REF=path  also time the reference: oracle/_ref/libjerasure_ref.so (test
+ *                        infrastructure: the real jerasure behind erasure_tools.c's dispatch)
+ *        FNPTR_ONLY_REF=1  time the reference only
  */
 #include <dlfcn.h>
 #include <pthread.h>
@@ -22,11 +31,25 @@
 
 #include "lstore_ec.h"
 
+#define MAX_SAMPLES 200000  /* latency samples kept per thread */
+
 static lio_erasure_plan_t *g_plan;
+static void *g_ref;  /* ref_plan_t* of oracle/_ref */
+static void (*g_ref_encode)(void *, char **, int);
+static int (*g_ref_decode)(void *, char **, int, int *);
 static int (*g_host_malloc)(void **, size_t, unsigned);
 static int (*g_host_free)(void *);
-static int g_chunk, g_calls;
-static double *g_lat;
+static int g_chunk, g_decode, g_use_ref, g_k = 6, g_m = 3;
+static double g_seconds;
+static volatile double g_t_end;
+static pthread_barrier_t g_bar;
+
+typedef struct {
+    long t;
+    long calls;
+    double *lat;
+    long nlat;
+} thread_rec_t;
 
 static double now(void)
 {
@@ -35,27 +58,50 @@ static double now(void)
     return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
+static void one_call(char **ptr, int *erasures)
+{
+    if (g_use_ref) {
+        if (g_decode) g_ref_decode(g_ref, ptr, g_chunk, erasures);
+        else g_ref_encode(g_ref, ptr, g_chunk);
+    } else {
+        if (g_decode) g_plan->decode_block(g_plan, ptr, g_chunk, erasures);   /* segment/jerasure.c:245 */
+        else g_plan->encode_block(g_plan, ptr, g_chunk);                      /* segment/jerasure.c:1847 */
+    }
+}
+
 static void *worker(void *arg)
 {
-    long t = (long)arg;
-    int k = g_plan->data_strips, m = g_plan->parity_strips;
+    thread_rec_t *r = (thread_rec_t *)arg;
+    int k = g_k, m = g_m;
     char *buf = NULL;
     if (g_host_malloc) {
         if (g_host_malloc((void **)&buf, (size_t)(k + m) * g_chunk, 0) != 0) buf = NULL;
     } else {
         buf = malloc((size_t)(k + m) * g_chunk);
     }
-    if (!buf) return NULL;
-    char *ptr[64];
-    for (size_t i = 0; i < (size_t)(k + m) * g_chunk; i++) buf[i] = (char)(i * 131 + t);
-    for (int i = 0; i < k + m; i++) ptr[i] = buf + (size_t)i * g_chunk;
-    for (int c = 0; c < g_calls; c++) {
-        double t0 = now();
-        g_plan->encode_block(g_plan, ptr, g_chunk);     /* segment/jerasure.c:1847 */
-        g_lat[t * g_calls + c] = now() - t0;
+    char *ptr[256];
+    int erasures[2] = {0, -1};
+    if (buf) {
+        for (size_t i = 0; i < (size_t)(k + m) * g_chunk; i++) buf[i] = (char)(i * 131 + r->t);
+        for (int i = 0; i < k + m; i++) ptr[i] = buf + (size_t)i * g_chunk;
+        if (g_use_ref) g_ref_encode(g_ref, ptr, g_chunk);   /* consistent parity for the decodes */
+        else g_plan->encode_block(g_plan, ptr, g_chunk);
+        for (int c = 0; c < 3; c++) one_call(ptr, erasures);  /* warm */
     }
-    if (g_host_malloc) g_host_free(buf);
-    else free(buf);
+    pthread_barrier_wait(&g_bar);  /* timed phase starts */
+    while (buf) {
+        double t0 = now();
+        one_call(ptr, erasures);
+        double t1 = now();
+        if (r->nlat < MAX_SAMPLES) r->lat[r->nlat++] = t1 - t0;
+        r->calls++;
+        if (t1 >= g_t_end) break;
+    }
+    pthread_barrier_wait(&g_bar);  /* timed phase ends */
+    if (buf) {
+        if (g_host_malloc) g_host_free(buf);
+        else free(buf);
+    }
     return NULL;
 }
 
@@ -63,6 +109,49 @@ static int cmp(const void *a, const void *b)
 {
     double x = *(const double *)a, y = *(const double *)b;
     return x < y ? -1 : x > y;
+}
+
+static void run(int T, const char *impl, const char *method)
+{
+    pthread_t th[1024];
+    thread_rec_t rec[1024];
+    pthread_barrier_init(&g_bar, NULL, T + 1);
+    for (long t = 0; t < T; t++) {
+        rec[t].t = t;
+        rec[t].calls = 0;
+        rec[t].nlat = 0;
+        rec[t].lat = malloc(sizeof(double) * MAX_SAMPLES);
+        pthread_create(&th[t], NULL, worker, &rec[t]);
+    }
+    g_t_end = now() + 1e9;
+    pthread_barrier_wait(&g_bar);  /* every thread warmed up */
+    double t0 = now();
+    g_t_end = t0 + g_seconds;
+    pthread_barrier_wait(&g_bar);  /* every thread done */
+    double wall = now() - t0;
+    long calls = 0, n = 0;
+    for (int t = 0; t < T; t++) {
+        pthread_join(th[t], NULL);
+        calls += rec[t].calls;
+        n += rec[t].nlat;
+    }
+    double *lat = malloc(sizeof(double) * (n ? n : 1));
+    long o = 0;
+    for (int t = 0; t < T; t++) {
+        memcpy(lat + o, rec[t].lat, sizeof(double) * rec[t].nlat);
+        o += rec[t].nlat;
+        free(rec[t].lat);
+    }
+    qsort(lat, n, sizeof(double), cmp);
+    pthread_barrier_destroy(&g_bar);
+    const char *sp = getenv("LSEC_SMALL_PATH");
+    printf("{\"impl\": \"%s\", \"op\": \"%s\", \"chunk\": %d, \"threads\": %d, \"calls\": %ld, \"seconds\": %.3f, "
+           "\"method\": \"%s\", \"pinned\": %d, \"small_path\": \"%s\", \"per_call_us_p50\": %.1f, "
+           "\"per_call_us_p99\": %.1f, \"gibps\": %.3f}\n",
+           impl, g_decode ? "decode" : "encode", g_chunk, T, calls, wall, method, g_host_malloc != NULL, sp ? sp : "default",
+           n ? lat[n / 2] * 1e6 : 0.0, n ? lat[(size_t)(n * 0.99)] * 1e6 : 0.0, calls * (double)g_k * g_chunk / wall / (1 << 30));
+    fflush(stdout);
+    free(lat);
 }
 
 int main(int argc, char **argv)
@@ -80,34 +169,32 @@ int main(int argc, char **argv)
     }
     g_chunk = argc > 1 ? atoi(argv[1]) : 16384;
     int T = argc > 2 ? atoi(argv[2]) : 8;
-    g_calls = argc > 3 ? atoi(argv[3]) : 200;
+    g_seconds = argc > 3 ? atof(argv[3]) : 2.0;
     int method = argc > 4 ? et_method_type(argv[4]) : CAUCHY_GOOD;
-    int k = 6, m = 3;
-    g_plan = et_generate_plan((long long)k * g_chunk, method, k, m, -1, -1, -1);   /* :2237 */
+    g_decode = argc > 5 && strcmp(argv[5], "decode") == 0;
+    if (T > 1024) T = 1024;
+    if (T < 1) T = 1;
+    g_plan = et_generate_plan((long long)g_k * g_chunk, method, g_k, g_m, -1, -1, -1);   /* :2237 */
     if (!g_plan || g_plan->form_encoding_matrix(g_plan) || g_plan->form_decoding_matrix(g_plan)) {
         fprintf(stderr, "plan: %s\n", lsec_last_error());
         return 1;
     }
-    g_lat = calloc((size_t)T * g_calls, sizeof(double));
-    pthread_t th[1024];
-    { /* warm: staging, dispatcher, device images */
-        g_calls = 2;
-        for (long t = 0; t < T; t++) pthread_create(&th[t], NULL, worker, (void *)t);
-        for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
-        g_calls = argc > 3 ? atoi(argv[3]) : 200;
+    const char *only_ref = getenv("FNPTR_ONLY_REF");
+    if (!(only_ref && atoi(only_ref))) run(T, "engine", JE_method[method]);
+    const char *ref_so = getenv("FNPTR_REF");
+    if (ref_so && *ref_so) {
+        void *h = dlopen(ref_so, RTLD_NOW | RTLD_LOCAL);
+        void *(*ref_new)(int, int, int, int, int) = h ? (void *(*)(int, int, int, int, int))dlsym(h, "ref_plan_new") : NULL;
+        g_ref_encode = h ? (void (*)(void *, char **, int))dlsym(h, "ref_plan_encode") : NULL;
+        g_ref_decode = h ? (int (*)(void *, char **, int, int *))dlsym(h, "ref_plan_decode") : NULL;
+        if (!ref_new || !g_ref_encode || !g_ref_decode) {
+            fprintf(stderr, "FNPTR_REF: cannot load %s\n", ref_so);
+            return 1;
+        }
+        g_ref = ref_new(method, g_k, g_m, g_plan->w, g_plan->packet_size);
+        g_use_ref = 1;
+        run(T, "reference", JE_method[method]);
     }
-    double t0 = now();
-    for (long t = 0; t < T; t++) pthread_create(&th[t], NULL, worker, (void *)t);
-    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
-    double wall = now() - t0;
-    size_t n = (size_t)T * g_calls;
-    qsort(g_lat, n, sizeof(double), cmp);
-    const char *kc = getenv("LSEC_KERNEL_COPY");
-    printf("{\"chunk\": %d, \"threads\": %d, \"calls\": %zu, \"method\": \"%s\", \"pinned\": %d, \"kernel_copy\": \"%s\", "
-           "\"per_call_us_p50\": %.1f, \"per_call_us_p99\": %.1f, \"gibps\": %.3f}\n", g_chunk, T, n, JE_method[method],
-           g_host_malloc != NULL, kc ? kc : "default",
-           g_lat[n / 2] * 1e6, g_lat[(size_t)(n * 0.99)] * 1e6, n * (double)k * g_chunk / wall / (1 << 30));
     et_destroy_plan(g_plan);
-    free(g_lat);
     return 0;
 }
