@@ -127,7 +127,7 @@ def main():
         par = rp.encode(data)
         full = np.vstack([data, par])
         dec = []
-        if size <= (1 << 20):
+        if size <= (4 << 20):  # every geometry up to c4's 4 MiB chunks
             for er in erasure_sets(k, m):
                 sh = full.copy()
                 for e in er:
@@ -136,7 +136,10 @@ def main():
                 ok = bool((sh == full).all())
                 if meth == O.RAID4 and rc == 0 and all(e >= k for e in er):
                     ok = None  # raid4_decode returns early on parity loss (raid4.c:52)
-                dec.append(dict(erasures=er, rc=int(rc), recovered=ok))
+                ent = dict(erasures=er, rc=int(rc), recovered=ok)
+                if rc == 0:  # CRC32 of what the reference rebuilt, erased shards in ascending order
+                    ent["rebuilt_crc32"] = ["%08x" % zlib.crc32(sh[e].tobytes()) for e in sorted(set(er))]
+                dec.append(ent)
         rp.close()
         key = None
         if size * m <= 12 * 1024:

@@ -55,6 +55,19 @@ def test_oracle_decode_matches_golden(built, golden):
             assert rc == d["rc"], (v["name"], d)
             if rc == 0 and d["recovered"]:
                 assert np.array_equal(sh, full)
+            if rc == 0 and "rebuilt_crc32" in d and d["recovered"] is not None:
+                got = ["%08x" % zlib.crc32(sh[e].tobytes()) for e in sorted(set(d["erasures"]))]
+                assert got == d["rebuilt_crc32"], (v["name"], d["erasures"])
+
+
+def test_golden_decode_covers_c4(golden):
+    """The fixtures hold the reference's decodes at the c4 geometry (Cauchy-good 10+4 and RS 10+4,
+    C = 4 MiB): every erasure pattern, with the CRC32 of the shards it rebuilt."""
+    c4 = [v for v in golden["vectors"] if v["k"] == 10 and v["m"] == 4 and v["size"] == 4 << 20]
+    assert {v["name"] for v in c4} == {"cauchy_good", "reed_sol_van"}
+    for v in c4:
+        ok = [d for d in v["decode"] if d["rc"] == 0]
+        assert len(ok) >= 9 and all(d["recovered"] and d["rebuilt_crc32"] for d in ok)
 
 
 # SURVEY.md §8c known-answer anchors (first 16 parity bytes / CRC32 per parity chunk)
