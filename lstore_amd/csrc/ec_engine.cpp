@@ -35,6 +35,7 @@
 #include "../../include/lstore_ec.h"
 #include "ec_host.h"
 #include "ec_kernels.h"
+#include "ec_server.h"
 #include "gf8.h"
 
 using lsec::CoefCell;
@@ -1733,20 +1734,15 @@ struct ZcSlot {  // one calling thread's page-locked slot on one device
 // on the flag (a flag seen ~8 us sooner than hipStreamSynchronize returns:
 // tools/probes/zc_probe.hip, profiles/r02_v3_zc_probe.txt).  A call whose flag has not come
 // after a second falls back to the stream's own status, so a failed launch is reported.
+bool wait_flag(const unsigned *flag, unsigned v, hipStream_t st, int *rc);
+
 int zc_complete(ZcSlot &sl, hipStream_t st) {
   const unsigned v = ++sl.seq == 0 ? ++sl.seq : sl.seq;
   const hipError_t e = lsec::launch_signal(sl.counter, sl.dflag, v, st);
   if (e != hipSuccess) return fail("signal launch: %s", hipGetErrorString(e));
-  const auto t0 = std::chrono::steady_clock::now();
-  for (unsigned spins = 0; __atomic_load_n(sl.flag, __ATOMIC_ACQUIRE) != v; ++spins) {
-    __builtin_ia32_pause();
-    if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
-      HIP_OK(hipStreamSynchronize(st));
-      if (__atomic_load_n(sl.flag, __ATOMIC_ACQUIRE) != v) return fail("zero-copy call: completion flag never came");
-      break;
-    }
-  }
-  return 0;
+  int rc = 0;
+  wait_flag(sl.flag, v, st, &rc);
+  return rc;
 }
 
 // regular stripe stride of device addresses a[s * per + i] (i < per): shard i of stripe s at
@@ -1759,6 +1755,286 @@ bool regular_refs(const std::vector<uint64_t> &a, int nstripes, size_t per, std:
     for (size_t i = 0; i < per; ++i)
       if (a[s * per + i] != a[i] + static_cast<uint64_t>(s * stride[i])) return false;
   return true;
+}
+
+// Waits until flag reaches v (wrapping u32 sequence): spin first (the usual call completes in
+// ~10-20 us), then yield, then sleep, so many waiting callers do not starve the one whose work
+// is done of a CPU.  Bounded: after `limit` the caller checks its stream for an error.
+bool wait_flag(const unsigned *flag, unsigned v, hipStream_t st, int *rc) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spins = 0;; ++spins) {
+    if (static_cast<int>(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - v) >= 0) return true;
+    if (spins < 500) {
+      __builtin_ia32_pause();
+      continue;
+    }
+    const auto dt = std::chrono::steady_clock::now() - t0;
+    if (dt > std::chrono::seconds(2)) {
+      const hipError_t e = hipStreamSynchronize(st);
+      if (static_cast<int>(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - v) >= 0) return true;
+      *rc = fail("zero-copy call: completion flag never came (%s)", hipGetErrorString(e));
+      return false;
+    }
+    if (dt < std::chrono::microseconds(200)) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+// ---------------------------------------------------------------- stripe server (host side)
+// Per-stripe calls up to kSlotBytes per part are served by the persistent stripe server
+// (ec_server.hip): the calling thread claims slots, copies its chunks' column blocks into them
+// (or, for page-locked caller chunks, just names their device addresses), posts one descriptor
+// per part and spins on the parts' done flags.  No launch, no DMA and no other host thread per
+// call; the server's workgroups serve the parts of many callers in parallel.  The server exits
+// after 2 ms without work and is relaunched by the next caller (or by a waiting one that finds
+// it gone).  LSEC_SERVER=0 turns it off.
+class StripeServer {
+ public:
+  static StripeServer *for_device(int dev) {
+    static std::mutex m;
+    static std::map<int, StripeServer *> all;  // intentionally leaked: lives until exit
+    std::lock_guard<std::mutex> lk(m);
+    StripeServer *&r = all[dev];
+    if (!r) {
+      r = new StripeServer(dev);
+      registry().push_back(r);
+      static std::once_flag once;
+      std::call_once(once, [] { atexit(stop_all); });
+    }
+    return r;
+  }
+
+  // 0 served, -1 error, 1 not servable here (the caller takes another path)
+  int run(PlanExt *e, char **ptrs, long long C, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
+          const void *image, int kind, const CallerPinned *cp) {
+    const size_t nin = in_ids.size(), nout = out_ids.size(), nio = nin + nout;
+    if (nin < 1 || nout < 1 || nin > lsec::kSrvMaxK || nout > lsec::kSrvMaxR) return 1;
+    if (kind != KBYTEWISE && kind != KBITSLICED) return 1;
+    const lio_erasure_plan_t *p = &e->pub;
+    const bool direct = cp && cp->by_kernel;
+    // parts: column blocks of about 4 KiB per shard (one 256-lane x 16 B pass), whole
+    // super-packets for the bit-sliced layout, at most kMaxParts of them
+    const long long unit = kind == KBITSLICED ? 8LL * p->packet_size : 16;
+    const long long max_len = direct ? C : static_cast<long long>(kSlotBytes / nio) / unit * unit;
+    if (max_len < std::min<long long>(unit, C)) return 1;
+    long long len = std::min(std::max<long long>(unit, 4096 / unit * unit), max_len);
+    if ((C + len - 1) / len > kMaxParts) {
+      len = ((C + kMaxParts - 1) / kMaxParts + unit - 1) / unit * unit;
+      if (len > max_len) return 1;
+    }
+    if (len > C) len = C;
+    const int nparts = static_cast<int>((C + len - 1) / len);
+    int slot[kMaxParts];
+    if (!claim(nparts, slot)) return 1;
+    if (init_once()) {
+      release(nparts, slot);
+      return -1;
+    }
+    uint32_t want[kMaxParts];
+    for (int q = 0; q < nparts; ++q) {
+      const int sl = slot[q];
+      const long long c0 = static_cast<long long>(q) * len, n = std::min(len, C - c0);
+      lsec::SrvDesc &d = sh_->desc[sl];
+      d.kind = kind == KBITSLICED ? lsec::kSrvBitsliced : lsec::kSrvBytewise;
+      d.K = static_cast<uint32_t>(nin);
+      d.R = static_cast<uint32_t>(nout);
+      d.packet = static_cast<uint32_t>(p->packet_size);
+      d.size = static_cast<uint64_t>(n);
+      d.cells = reinterpret_cast<uint64_t>(image);
+      d.cstride = static_cast<uint32_t>(nin);
+      if (direct) {
+        for (size_t j = 0; j < nin; ++j) d.in[j] = cp->dev[j] + static_cast<uint64_t>(c0);
+        for (size_t r = 0; r < nout; ++r) d.out[r] = cp->dev[nin + r] + static_cast<uint64_t>(c0);
+      } else {
+        char *region = data_ + static_cast<size_t>(sl) * kSlotBytes;
+        const uint64_t dregion = data_dev_ + static_cast<uint64_t>(sl) * kSlotBytes;
+        for (size_t j = 0; j < nin; ++j) {
+          std::memcpy(region + j * n, ptrs[in_ids[j]] + c0, static_cast<size_t>(n));
+          d.in[j] = dregion + j * n;
+        }
+        for (size_t r = 0; r < nout; ++r) d.out[r] = dregion + (nin + r) * n;
+      }
+      want[q] = ++seq_[sl] == 0 ? ++seq_[sl] : seq_[sl];
+      __atomic_store_n(&sh_->post[lsec::srv_wg(sl)][lsec::srv_word(sl)], want[q], __ATOMIC_RELEASE);
+    }
+    const auto t_post = std::chrono::steady_clock::now();
+    int rc = ensure_running(false);
+    const auto t0 = std::chrono::steady_clock::now();
+    auto last_check = t0;
+    for (int q = 0; q < nparts && rc == 0; ++q) {
+      const uint32_t *flag = &sh_->done[slot[q]][0];
+      for (unsigned spins = 0; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != want[q]; ++spins) {
+        if (spins < 500) {
+          __builtin_ia32_pause();
+          continue;
+        }
+        const auto now = std::chrono::steady_clock::now();
+        if (now - last_check > std::chrono::microseconds(100)) {  // did the server retire meanwhile?
+          last_check = now;
+          if ((rc = ensure_running(true))) break;
+        }
+        if (now - t0 > std::chrono::seconds(5)) {
+          rc = fail("stripe server: no answer for 5 s");
+          broken_ = true;
+          break;
+        }
+        if (now - t0 < std::chrono::microseconds(200)) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
+      }
+    }
+    static const bool trace = getenv("LSEC_TRACE") != nullptr;
+    if (trace) {  // calls slower than 1 ms: where the time went
+      const auto t_end = std::chrono::steady_clock::now();
+      const auto us = [](std::chrono::steady_clock::duration d) { return std::chrono::duration<double, std::micro>(d).count(); };
+      if (t_end - t_post > std::chrono::milliseconds(1))
+        fprintf(stderr, "[lsec trace] server call %d parts (slots %d..): ensure %.1f us, wait %.1f us, rc %d\n", nparts, slot[0],
+                us(t0 - t_post), us(t_end - t0), rc);
+    }
+    if (rc == 0)
+      last_seen_us_.store(std::chrono::duration_cast<std::chrono::microseconds>(
+                              std::chrono::steady_clock::now().time_since_epoch()).count(),
+                          std::memory_order_relaxed);
+    if (rc == 0 && !direct)
+      for (int q = 0; q < nparts; ++q) {
+        const long long c0 = static_cast<long long>(q) * len, n = std::min(len, C - c0);
+        const char *region = data_ + static_cast<size_t>(slot[q]) * kSlotBytes;
+        for (size_t r = 0; r < nout; ++r) std::memcpy(ptrs[out_ids[r]] + c0, region + (nin + r) * n, static_cast<size_t>(n));
+      }
+    if (rc == 0) release(nparts, slot);  // a slot whose post may still be served is never handed out again
+    return rc;
+  }
+
+ private:
+  static constexpr size_t kSlotBytes = 96u << 10;  // chunk bytes of one part (inputs + outputs)
+  static constexpr int kMaxParts = 16;
+
+  explicit StripeServer(int dev) : dev_(dev) {
+    for (auto &b : busy_) b.store(0);
+    for (auto &q : seq_) q = 0;
+  }
+
+  static std::vector<StripeServer *> &registry() {
+    // leaked: stop_all runs from atexit and must find it intact (a function-local static
+    // constructed after the atexit registration would be destroyed before stop_all runs)
+    static std::vector<StripeServer *> *r = new std::vector<StripeServer *>();
+    return *r;
+  }
+  // at exit: stop every running server and let it drain (its stop word is read on every idle poll)
+  static void stop_all() {
+    for (StripeServer *s : registry()) {
+      std::lock_guard<std::mutex> lk(s->mu_);
+      if (!s->sh_ || !s->running_) continue;
+      for (int g = 0; g < lsec::kSrvWG; ++g) __atomic_store_n(&s->sh_->post[g][lsec::kSrvSlotsPerWG], 1u, __ATOMIC_RELEASE);
+      (void)hipEventSynchronize(s->ev_);
+      s->running_ = false;
+    }
+  }
+
+  bool claim(int n, int *slot) {
+    static std::atomic<unsigned> next{0};
+    thread_local unsigned base = next.fetch_add(7919) % lsec::kSrvSlots;
+    int got = 0;
+    for (int k = 0; k < lsec::kSrvSlots && got < n; ++k) {
+      const int s = static_cast<int>((base + k) % lsec::kSrvSlots);
+      uint8_t z = 0;
+      if (busy_[s].compare_exchange_strong(z, 1)) slot[got++] = s;
+    }
+    if (got < n) {
+      release(got, slot);
+      return false;
+    }
+    return true;
+  }
+  void release(int n, const int *slot) {
+    for (int q = 0; q < n; ++q) busy_[slot[q]].store(0, std::memory_order_release);
+  }
+
+  int init_once() {
+    if (ready_.load(std::memory_order_acquire)) return 0;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (ready_.load()) return 0;
+    DeviceGuardLite g(dev_);
+    int lo = 0, hi = 0;
+    HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_OK(hipStreamCreateWithPriority(&st_, hipStreamNonBlocking, hi));  // a hardware queue of its own
+    HIP_OK(hipEventCreateWithFlags(&ev_, hipEventDisableTiming));
+    HIP_OK(hipMalloc(reinterpret_cast<void **>(&votes_), 64));
+    HIP_OK(hipMemset(votes_, 0, 64));
+    HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&sh_), sizeof(lsec::SrvShared), hipHostMallocCoherent));
+    std::memset(static_cast<void *>(sh_), 0, sizeof(lsec::SrvShared));
+    void *p = nullptr;
+    HIP_OK(hipHostGetDevicePointer(&p, sh_, 0));
+    sh_dev_ = reinterpret_cast<uint64_t>(p);
+    HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&data_), kSlotBytes * lsec::kSrvSlots, hipHostMallocCoherent));
+    HIP_OK(hipHostGetDevicePointer(&p, data_, 0));
+    data_dev_ = reinterpret_cast<uint64_t>(p);
+    ready_.store(true, std::memory_order_release);
+    return 0;
+  }
+
+  int ensure_running(bool check) {
+    // the server retires after 2 ms without work: past 1.5 ms since a part was last seen done,
+    // ask the runtime whether it is still there before relying on it
+    const int64_t now = std::chrono::duration_cast<std::chrono::microseconds>(
+                            std::chrono::steady_clock::now().time_since_epoch()).count();
+    if (!check && now - last_seen_us_.load(std::memory_order_relaxed) > 1500) check = true;
+    if (!check && running_.load(std::memory_order_acquire)) return 0;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (broken_) return fail("stripe server: unusable after an earlier failure");
+    if (running_ && check) {
+      const hipError_t q = hipEventQuery(ev_);
+      if (q == hipSuccess) running_ = false;
+      else if (q != hipErrorNotReady) return fail("stripe server: %s", hipGetErrorString(q));
+    }
+    if (running_) return 0;
+    for (int g = 0; g < lsec::kSrvWG; ++g) sh_->post[g][lsec::kSrvSlotsPerWG] = 0;  // stop word
+    lsec::SrvArgs a;
+    a.shared = reinterpret_cast<lsec::SrvShared *>(sh_dev_);
+    a.votes = votes_;
+    a.idle_ticks = 200000;  // 2 ms at the 100 MHz wall clock
+    DeviceGuardLite g(dev_);
+    hipError_t err = hipMemsetAsync(votes_, 0, sizeof(int), st_);
+    if (err == hipSuccess) err = lsec::launch_stripe_server(a, st_);
+    if (err == hipSuccess) err = hipEventRecord(ev_, st_);
+    if (err != hipSuccess) return fail("stripe server launch: %s", hipGetErrorString(err));
+    running_ = true;
+    return 0;
+  }
+
+  struct DeviceGuardLite {  // (DeviceGuard is defined further down)
+    int prev = -1;
+    explicit DeviceGuardLite(int dev) {
+      if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+      if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuardLite() {
+      if (prev >= 0) (void)hipSetDevice(prev);
+    }
+  };
+
+  int dev_;
+  lsec::SrvShared *sh_ = nullptr;
+  uint64_t sh_dev_ = 0;
+  char *data_ = nullptr;
+  uint64_t data_dev_ = 0;
+  std::atomic<uint8_t> busy_[lsec::kSrvSlots];
+  uint32_t seq_[lsec::kSrvSlots];
+  std::atomic<bool> ready_{false};
+  std::mutex mu_;
+  hipStream_t st_ = nullptr;
+  hipEvent_t ev_ = nullptr;
+  int *votes_ = nullptr;
+  std::atomic<bool> running_{false};
+  std::atomic<bool> broken_{false};
+  std::atomic<int64_t> last_seen_us_{0};
+};
+
+bool server_enabled() {
+  static const bool on = [] {
+    const char *s = getenv("LSEC_SERVER");
+    return !s || *s != '0';
+  }();
+  return on;
 }
 
 int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
@@ -1777,6 +2053,10 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
   if (!slot) slot.reset(new ZcSlot());
   if (slot->init_signal()) return -1;
   CallerPinned cp = caller_pinned(ptrs, nstripes, km, in_ids, out_ids, C, aligned);
+  if (nstripes == 1 && server_enabled()) {
+    const int rc = StripeServer::for_device(dev)->run(e, ptrs, C, in_ids, out_ids, image, kind, &cp);
+    if (rc != 1) return rc;
+  }
   std::vector<int64_t> stride;
   if (cp.by_kernel && regular_refs(cp.dev, nstripes, nio, stride)) {
     // caller page-locked chunks: read and written in place over PCIe

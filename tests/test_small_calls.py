@@ -1,0 +1,100 @@
+"""The small-call path LStore uses: plan->encode_block / plan->decode_block once per stripe from
+many pool threads (segment/jerasure.c:1847, :245, :1937).  Such calls are served zero-copy by
+the stripe server (ec_server.hip): the calling thread posts column parts of its stripe to a
+persistent kernel through page-locked slots, or names its own page-locked chunks.  Checked
+bit-exactly against the oracle from many threads at once, across the server's idle retirement
+and relaunch, with ragged chunk sizes, and across plans whose coefficient images reuse device
+addresses while the server runs.
+"""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import lstore_amd as L
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _pinned(shape):
+    import torch
+
+    return torch.empty(shape, dtype=torch.uint8, pin_memory=True).numpy()
+
+
+GEOS = [(L.REED_SOL_VAN, 6, 3, 16384), (L.CAUCHY_GOOD, 6, 3, 16384), (L.REED_SOL_VAN, 10, 4, 8200),
+        (L.CAUCHY_GOOD, 10, 4, 65536), (L.REED_SOL_VAN, 20, 6, 4096), (L.CAUCHY_ORIG, 4, 2, 2048),
+        (L.REED_SOL_R6_OP, 6, 2, 24576), (L.RAID4, 6, 1, 16384)]
+
+
+@pytest.mark.parametrize("method,k,m,C", GEOS)
+def test_single_calls_match_oracle(cuda, method, k, m, C):
+    with L.Plan.for_chunk(method, k, m, C) as p:
+        rng = np.random.default_rng(C + k)
+        R = 2 if method == L.REED_SOL_R6_OP else (1 if method == L.RAID4 else m)
+        for pinned in (False, True):
+            sh = _pinned((k + m, C)) if pinned else np.empty((k + m, C), np.uint8)
+            for it in range(4):
+                sh[:k] = rng.integers(0, 256, (k, C), dtype=np.uint8)
+                sh[k:] = 0x77
+                p.encode_block([sh[i] for i in range(k + m)])
+                want = O.encode(method, np.ascontiguousarray(sh[:k]), m, p.packet_size)
+                assert np.array_equal(sh[k:k + R], want[:R]), (pinned, it)
+                full = sh.copy()
+                lost = [it % k] if method == L.RAID4 else sorted({it % (k + m), (it * 5 + 1) % (k + m)})[:m]
+                sh[lost] = 0xEE
+                assert p.decode_block([sh[i] for i in range(k + m)], lost) == 0
+                assert np.array_equal(sh, full), (pinned, it, lost)
+
+
+def test_many_threads_mixed_plans_and_idle_gaps(cuda):
+    """32 threads over four plans, pageable and page-locked buffers, with pauses longer than the
+    server's 2 ms idle retirement so it is relaunched while others are mid-call."""
+    plans = [L.Plan.for_chunk(mth, k, m, C) for mth, k, m, C in GEOS[:4]]
+    errors = []
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(1000 + t)
+            p = plans[t % len(plans)]
+            mth, k, m, C = GEOS[t % len(plans)]
+            sh = _pinned((k + m, C)) if t % 3 == 0 else np.empty((k + m, C), np.uint8)
+            for it in range(12):
+                sh[:k] = rng.integers(0, 256, (k, C), dtype=np.uint8)
+                p.encode_block([sh[i] for i in range(k + m)])
+                if not np.array_equal(sh[k:], O.encode(mth, np.ascontiguousarray(sh[:k]), m, p.packet_size)):
+                    errors.append((t, it, "encode"))
+                full = sh.copy()
+                lost = [(t + it) % (k + m)]
+                sh[lost] = 0
+                if p.decode_block([sh[i] for i in range(k + m)], lost) != 0 or not np.array_equal(sh, full):
+                    errors.append((t, it, "decode"))
+                if it % 4 == 3:
+                    time.sleep(0.004 + 0.001 * (t % 3))
+        except Exception as ex:  # noqa: BLE001
+            errors.append((t, repr(ex)))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(32)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    for p in plans:
+        p.close()
+    assert not errors, errors[:8]
+
+
+def test_new_plans_while_the_server_runs(cuda):
+    """Plans are destroyed and created while the server keeps running: a new plan's coefficient
+    image may take a destroyed one's device address, and the server must read the new cells."""
+    C = 16384
+    rng = np.random.default_rng(5)
+    for round_ in range(12):
+        method, k, m = [(L.REED_SOL_VAN, 6, 3), (L.CAUCHY_GOOD, 6, 3), (L.REED_SOL_VAN, 4, 2)][round_ % 3]
+        with L.Plan.for_chunk(method, k, m, C) as p:
+            sh = np.empty((k + m, C), np.uint8)
+            sh[:k] = rng.integers(0, 256, (k, C), dtype=np.uint8)
+            p.encode_block([sh[i] for i in range(k + m)])
+            assert np.array_equal(sh[k:], O.encode(method, np.ascontiguousarray(sh[:k]), m, p.packet_size)), round_

@@ -143,13 +143,17 @@ static void run(int T, const char *impl, const char *method)
         free(rec[t].lat);
     }
     qsort(lat, n, sizeof(double), cmp);
+    double sum = 0;
+    for (long i = 0; i < n; i++) sum += lat[i];
     pthread_barrier_destroy(&g_bar);
     const char *sp = getenv("LSEC_SMALL_PATH");
     printf("{\"impl\": \"%s\", \"op\": \"%s\", \"chunk\": %d, \"threads\": %d, \"calls\": %ld, \"seconds\": %.3f, "
            "\"method\": \"%s\", \"pinned\": %d, \"small_path\": \"%s\", \"per_call_us_p50\": %.1f, "
-           "\"per_call_us_p99\": %.1f, \"gibps\": %.3f}\n",
+           "\"per_call_us_p99\": %.1f, \"per_call_us_p999\": %.1f, \"per_call_us_max\": %.1f, \"per_call_us_mean\": %.1f, "
+           "\"gibps\": %.3f}\n",
            impl, g_decode ? "decode" : "encode", g_chunk, T, calls, wall, method, g_host_malloc != NULL, sp ? sp : "default",
-           n ? lat[n / 2] * 1e6 : 0.0, n ? lat[(size_t)(n * 0.99)] * 1e6 : 0.0, calls * (double)g_k * g_chunk / wall / (1 << 30));
+           n ? lat[n / 2] * 1e6 : 0.0, n ? lat[(size_t)(n * 0.99)] * 1e6 : 0.0, n ? lat[(size_t)(n * 0.999)] * 1e6 : 0.0,
+           n ? lat[n - 1] * 1e6 : 0.0, n ? sum / n * 1e6 : 0.0, calls * (double)g_k * g_chunk / wall / (1 << 30));
     fflush(stdout);
     free(lat);
 }
