@@ -219,6 +219,7 @@ class HipEngine:
         self.stream = torch.cuda.current_stream()
         self.sh = self.stream.cuda_stream
         self.er = E._erasure_array([a.lost])
+        self.plan.prepare_encode()  # wide codes: wait for the plan's compiled XOR network
         self.plan.prepare_decode([a.lost])
         self.lib = E.lib()
         self.tensors = None

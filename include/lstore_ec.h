@@ -193,6 +193,13 @@ int lsec_segment_inspect(lio_erasure_plan_t *plan, char *buf, int nstripes, int 
 /* Pre-build (and cache on the current device) the decode matrix for one erasure pattern,
  * so the first lsec_decode_dev of that pattern does no host work.  0 / -1. */
 int lsec_prepare_decode(lio_erasure_plan_t *plan, const int *erasures);
+/* The same for the encode image.  For wide matrix codes (R*K >= 96 at w = 8) both also wait
+ * for the plan's run-time compiled XOR network (ec_jit.cpp); until it is ready the table
+ * kernel serves.  0 / -1. */
+int lsec_prepare_encode(lio_erasure_plan_t *plan);
+/* 1 when the encode (erasures == NULL) or the decode of that erasure pattern runs on a
+ * compiled XOR network on the current device, 0 otherwise. */
+int lsec_plan_jit(lio_erasure_plan_t *plan, const int *erasures);
 
 /* Devices that serve host-memory calls (et_*_stripes, et_*_magic, the plan's fn-pointers,
  * lsec_segment_write).  n = 0 (the default): the calling thread's current HIP device.  With a

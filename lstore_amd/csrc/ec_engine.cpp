@@ -34,6 +34,7 @@
 
 #include "../../include/lstore_ec.h"
 #include "ec_host.h"
+#include "ec_jit.h"
 #include "ec_kernels.h"
 #include "ec_server.h"
 #include "gf8.h"
@@ -371,6 +372,8 @@ int encode_cells(PlanExt *e, const void **out) {
   CoefCell *d = nullptr;
   if (upload_cells(h, &d)) return -1;
   e->impl->enc_cells[dev] = d;
+  if (kernel_kind(e->pub.method, e->pub.w) == KBYTEWISE)  // wide codes: an XOR network, compiled in the background
+    lsec::jit::bind(d, e->impl->coding.data(), rows, k);
   *out = d;
   return 0;
 }
@@ -449,6 +452,8 @@ int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, con
     CoefCell *d = nullptr;
     if (upload_cells(h, &d)) return -1;
     dc = ent.dev_cells.emplace(dev, d).first;
+    if (!ent.xor_only && kernel_kind(e->pub.method, e->pub.w) == KBYTEWISE)
+      lsec::jit::bind(d, ent.dp.rows.data(), static_cast<int>(ent.dp.erased.size()), e->pub.data_strips);
   }
   *out = &ent;
   *cells = dc->second;
@@ -486,6 +491,21 @@ int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
 // KBITMATRIX the uint32 row masks [(r*w+l)*K + j].
 int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in, const ShardRef *out,
                   int nstripes, long long size, int packet, hipStream_t st, int w = 8) {
+  if (kind == KBYTEWISE && lsec::bytewise_variant() == 0 && lsec::jit::wants_xornet(R, K)) {
+    if (hipFunction_t fn = lsec::jit::ready(image, R, K)) {  // the matrix's compiled XOR network
+      // batches split so tile indices stay 32-bit, as below
+      const long long per = std::max(1LL, (1LL << 30) / std::max(1LL, size / 4096 + 1));
+      ShardRef bi[lsec::jit::kMaxCols], bo[lsec::jit::kMaxRows];
+      for (int s0 = 0; s0 < nstripes; s0 += static_cast<int>(std::min<long long>(per, nstripes))) {
+        const int n = static_cast<int>(std::min<long long>(per, nstripes - s0));
+        for (int j = 0; j < K; ++j) bi[j] = {in[j].base + static_cast<uint64_t>(s0) * in[j].stride, in[j].stride};
+        for (int r = 0; r < R; ++r) bo[r] = {out[r].base + static_cast<uint64_t>(s0) * out[r].stride, out[r].stride};
+        const hipError_t err = lsec::jit::launch(fn, R, K, bi, bo, n, size, st);
+        if (err != hipSuccess) return fail("xor network launch failed: %s", hipGetErrorString(err));
+      }
+      return 0;
+    }
+  }
   const int rmax = kind == KBITMATRIX ? 2 : ((kind == KBITSLICEDW || kind == KWORDWISE) && w == 32) ? 4 : 8;
   for (int r0 = 0; r0 < R; r0 += rmax) {
     lsec::ApplyArgs a;
@@ -2709,6 +2729,7 @@ void et_destroy_plan(lio_erasure_plan_t *p) {
     int cur = -1;
     (void)hipGetDevice(&cur);
     for (auto &kv : e->impl->enc_cells) {
+      lsec::jit::unbind(kv.second);  // before the address can be handed out again
       (void)hipSetDevice(kv.first);
       (void)hipFree(kv.second);
     }
@@ -2718,6 +2739,7 @@ void et_destroy_plan(lio_erasure_plan_t *p) {
     }
     for (auto &ent : e->impl->decode_cache) {
       for (auto &kv : ent.second.dev_cells) {
+        lsec::jit::unbind(kv.second);
         (void)hipSetDevice(kv.first);
         (void)hipFree(kv.second);
       }
@@ -3043,7 +3065,35 @@ int lsec_prepare_decode(lio_erasure_plan_t *plan, const int *erasures) {
   if (pr != 0) return pr < 0 ? -1 : 0;
   DecodeEntry *ent = nullptr;
   const void *cells = nullptr;
-  return decode_entry(e, ids, &ent, &cells);
+  if (decode_entry(e, ids, &ent, &cells)) return -1;
+  (void)lsec::jit::wait(cells, 30000);  // a wide code's XOR network, if it has one
+  return 0;
+}
+
+int lsec_prepare_encode(lio_erasure_plan_t *plan) {
+  PlanExt *e = ext_of(plan);
+  if (!e) return fail("not an lstore_ec plan");
+  const void *cells = nullptr;
+  if (encode_cells(e, &cells)) return -1;
+  (void)lsec::jit::wait(cells, 30000);
+  return 0;
+}
+
+int lsec_plan_jit(lio_erasure_plan_t *plan, const int *erasures) {
+  PlanExt *e = ext_of(plan);
+  if (!e || kernel_kind(e->pub.method, e->pub.w) != KBYTEWISE || lsec::bytewise_variant() != 0) return 0;
+  const void *cells = nullptr;
+  int R = 0;
+  if (!erasures) {
+    if (encode_cells(e, &cells)) return 0;
+    R = encode_rows(e);
+  } else {
+    std::vector<int> ids;
+    DecodeEntry *ent = nullptr;
+    if (parse_erasures(plan, erasures, ids) != 0 || decode_entry(e, ids, &ent, &cells)) return 0;
+    R = static_cast<int>(ent->dp.erased.size());
+  }
+  return lsec::jit::ready(cells, R, plan->data_strips) != nullptr ? 1 : 0;
 }
 
 int lsec_set_host_devices(const int *devices, int n) {

@@ -1,0 +1,405 @@
+// ec_jit.cpp -- per-matrix XOR networks for wide GF(2^8) matrix codes, compiled at run time
+// with hipRTC for gfx950.
+//
+// The bytewise kernel (ec_kernels_impl.h) multiplies by a coefficient with three v_perm_b32
+// table lookups per 4 bytes, about 5 VALU ops per (output, input) pair and dword.  Wide codes
+// are VALU-bound that way: RS(20+6) encode ran at 0.61-0.65 of 8 TB/s, 97 % VALU-busy
+// (DESIGN.md §3).  With the matrix known when the kernel is compiled, output r is a fixed
+// network evaluated in Horner form over the coefficient bits,
+//     out_r = x(...x(x S_r7 + S_r6)...) + S_r0,   S_rt = XOR of the inputs j whose A[r][j] has
+//     bit t set,
+// on 4 packed bytes per dword: multiplying by x is a shift plus 0x1D times the bit-7 flags (a
+// packed 16-bit multiply; 5 VALU ops), the S_rt are 3-input XORs (v_bitop3) -- straight-line
+// code, no table lookups, no branches.  For RS(20+6), with the 6-op shift-and-subtract doubling
+// (variant bit 1), that is 469 VALU instructions per dword column against 634 for the table
+// kernel (SQ_INSTS_VALU per wave 1875 vs 2537, profiles/r02_v14_pmc_valu_rs206.txt); the
+// packed multiply takes 7 % more off (offline count, tools/jit_variants.py).  Encode goes from
+// 0.67 to 0.73-0.74 of 8 TB/s.
+// (A bit-sliced form of the same Horner chains needs 8 x 8 bit transposes, 150 ops per dword,
+// and 300 VGPRs; it lost: profiles/r02_kbench_jit_v1.txt.)  Used for R * K >= 96 only: on
+// narrower codes the table kernel is already at the memory-bound rate.  The generated kernel
+// computes the same GF(2^8) products as the table kernel, bit for bit; it is used once its
+// compile has finished (in the background), and the table kernel serves until then.
+// LSEC_JIT=0 turns it off.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ec_host.h"
+#include "ec_jit.h"
+
+namespace lsec {
+namespace jit {
+
+namespace {
+
+// a balanced left fold of terms with 3-input XORs (ceil((n-1)/2) ops)
+std::string xor_chain(std::vector<std::string> t) {
+  if (t.empty()) return "0u";
+  while (t.size() > 1) {
+    std::vector<std::string> n;
+    size_t i = 0;
+    for (; i + 3 <= t.size(); i += 3) n.push_back("X3(" + t[i] + "," + t[i + 1] + "," + t[i + 2] + ")");
+    if (t.size() - i == 2) n.push_back("(" + t[i] + "^" + t[i + 1] + ")");
+    else if (t.size() - i == 1) n.push_back(t[i]);
+    t.swap(n);
+  }
+  return t[0];
+}
+
+}  // namespace
+
+bool wants_xornet(int R, int K) {
+  static const bool on = [] {
+    const char *s = getenv("LSEC_JIT");
+    return !s || *s != '0';
+  }();
+  return on && R >= 2 && R <= kMaxRows && K >= 2 && K <= kMaxCols && R * K >= 96;
+}
+
+// Code shape knobs (LSEC_JIT_VARIANT, read once; A/B runs): bit 0 = common-pair elimination,
+// bit 1 = doubling by shift-and-subtract instead of a packed 16-bit multiply, bits 4-7 = dwords
+// per lane (1, 2, 4; 0 = 4).  Measured on RS(20+6) (profiles/r02_v15_jit_ab.txt): all shapes
+// within 70.6-74.3 % of 8 TB/s, the default (4 dwords, packed multiply, no pair elimination)
+// best; pair elimination cuts VALU instructions 20 % but not time.
+int jit_variant() {
+  static const int v = [] {
+    const char *s = getenv("LSEC_JIT_VARIANT");
+    return s ? atoi(s) : 0;
+  }();
+  return v;
+}
+
+namespace {
+
+// One Horner step's XOR set: the inputs (or shared pairs) whose coefficient has bit t set.
+struct Step {
+  bool doubled;            // h = x * h first (every step after the top one)
+  std::vector<int> terms;  // symbol ids: 0..K-1 inputs, K.. shared pairs
+};
+
+// Greedy common-pair elimination over all steps of all rows (Paar's heuristic): the pair of
+// symbols that occurs together in the most XOR sets becomes a new symbol while it occurs in at
+// least 3 (one 2-input XOR then saves a term in each of them).
+void share_pairs(std::vector<std::vector<Step>> &rows, int K, std::vector<std::pair<int, int>> &pairs) {
+  for (;;) {
+    std::map<std::pair<int, int>, int> count;
+    for (auto &row : rows)
+      for (auto &st : row) {
+        std::vector<int> t = st.terms;
+        std::sort(t.begin(), t.end());
+        for (size_t i = 0; i < t.size(); ++i)
+          for (size_t j = i + 1; j < t.size(); ++j) ++count[{t[i], t[j]}];
+      }
+    std::pair<int, int> best{-1, -1};
+    int n = 0;
+    for (auto &kv : count)
+      if (kv.second > n) {
+        n = kv.second;
+        best = kv.first;
+      }
+    if (n < 3) return;
+    const int sym = K + static_cast<int>(pairs.size());
+    pairs.push_back(best);
+    for (auto &row : rows)
+      for (auto &st : row) {
+        auto a = std::find(st.terms.begin(), st.terms.end(), best.first);
+        auto b = std::find(st.terms.begin(), st.terms.end(), best.second);
+        if (a == st.terms.end() || b == st.terms.end()) continue;
+        st.terms.erase(std::remove_if(st.terms.begin(), st.terms.end(),
+                                      [&](int x) { return x == best.first || x == best.second; }),
+                       st.terms.end());
+        st.terms.push_back(sym);
+      }
+  }
+}
+
+}  // namespace
+
+std::string xornet_source(const uint8_t *mat, int R, int K) {
+  const int var = jit_variant();
+  // dwords per lane (16 B loads by default)
+  int D = (var >> 4) & 15;
+  if (D != 1 && D != 2 && D != 4) D = 4;
+  const int IT = D == 4 && K * 8 <= 104 ? 2 : 1;  // 16 B pieces per lane per shard (D = 4)
+  const int lane_bytes = 4 * D * IT;
+  const int tile = 256 * lane_bytes;
+  // the Horner steps of every row, then the shared pairs
+  std::vector<std::vector<Step>> rows(R);
+  for (int r = 0; r < R; ++r) {
+    int top = -1;
+    for (int t = 7; t >= 0 && top < 0; --t)
+      for (int j = 0; j < K; ++j)
+        if ((mat[r * K + j] >> t) & 1) top = t;
+    for (int t = top; t >= 0; --t) {
+      Step st;
+      st.doubled = t != top;
+      for (int j = 0; j < K; ++j)
+        if ((mat[r * K + j] >> t) & 1) st.terms.push_back(j);
+      rows[r].push_back(st);
+    }
+  }
+  std::vector<std::pair<int, int>> pairs;
+  if (var & 1) share_pairs(rows, K, pairs);
+  auto sym = [&](int x) { return (x < K ? "e" : "p") + std::to_string(x < K ? x : x - K) + "[d]"; };
+
+  std::ostringstream s;
+  s << "typedef unsigned int u32;\n"
+       "typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));\n"
+       "typedef u32 u32x4 __attribute__((ext_vector_type(4)));\n"
+       "typedef u32 u32x2 __attribute__((ext_vector_type(2)));\n"
+       "struct Ref { unsigned long long base; long long stride; };\n"
+    << "struct Args { long long size; int nstripes; int pad; Ref in[" << K << "]; Ref out[" << R << "]; };\n"
+    << "#define X3(a,b,c) __builtin_amdgcn_bitop3_b32((a),(b),(c),0x96)\n";
+  if (!(var & 2)) {
+    // x * (4 packed GF(2^8) elements), polynomial 0x11D: shift, and 0x1D times the bit-7 flags
+    // by a packed 16-bit multiply (each 16-bit half holds two flags, 0x1D1D at most)
+    s << "__device__ static inline u32 XT(u32 a) {\n"
+         "  const u16x2 f = __builtin_bit_cast(u16x2, (a >> 7) & 0x01010101u) * (u16x2){0x1D, 0x1D};\n"
+         "  return ((a << 1) & 0xFEFEFEFEu) ^ __builtin_bit_cast(u32, f);\n"
+         "}\n";
+  } else {
+    // x * (4 packed GF(2^8) elements), polynomial 0x11D: shift the low 7 bits of every byte,
+    // and XOR the taps 0x1D into the bytes whose bit 7 was set (t - (t >> 7) is 0x7F in exactly
+    // those bytes, borrow-free).  A 24-bit multiply of the bit-7 flags by 0x1D would drop byte 3.
+    s << "__device__ static inline u32 XT(u32 a) {\n"
+         "  const u32 t = a & 0x80808080u;\n"
+         "  return ((a ^ t) << 1) ^ ((t - (t >> 7)) & 0x1D1D1D1Du);\n"
+         "}\n";
+  }
+  s << "#define G(a) ((const __attribute__((address_space(1))) u32x4 *)(a))\n"
+       "#define GW(a) ((__attribute__((address_space(1))) u32x4 *)(a))\n"
+       "#define G2(a) ((const __attribute__((address_space(1))) u32x2 *)(a))\n"
+       "#define GW2(a) ((__attribute__((address_space(1))) u32x2 *)(a))\n"
+       "#define G1(a) ((const __attribute__((address_space(1))) u32 *)(a))\n"
+       "#define GW1(a) ((__attribute__((address_space(1))) u32 *)(a))\n"
+       // a lane's D dwords at byte o of a shard of C bytes (C % 8 == 0: tails are whole 8 B)
+       "__device__ static inline void ld4(u32 *e, unsigned long long p, long long o, long long C) {\n"
+       "  if (o + 16 <= C) { const u32x4 v = __builtin_nontemporal_load(G(p + o)); e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w; return; }\n"
+       "  e[0] = e[1] = e[2] = e[3] = 0u;\n"
+       "  if (o + 8 <= C) { const u32x2 h = *G2(p + o); e[0] = h.x; e[1] = h.y; }\n"
+       "}\n"
+       "__device__ static inline void st4(const u32 *h, unsigned long long p, long long o, long long C) {\n"
+       "  if (o + 16 <= C) __builtin_nontemporal_store((u32x4){h[0], h[1], h[2], h[3]}, GW(p + o));\n"
+       "  else if (o + 8 <= C) *GW2(p + o) = (u32x2){h[0], h[1]};\n"
+       "}\n"
+       "__device__ static inline void ld2(u32 *e, unsigned long long p, long long o, long long C) {\n"
+       "  if (o + 8 <= C) { const u32x2 v = __builtin_nontemporal_load(G2(p + o)); e[0] = v.x; e[1] = v.y; return; }\n"
+       "  e[0] = e[1] = 0u;\n"
+       "}\n"
+       "__device__ static inline void st2(const u32 *h, unsigned long long p, long long o, long long C) {\n"
+       "  if (o + 8 <= C) __builtin_nontemporal_store((u32x2){h[0], h[1]}, GW2(p + o));\n"
+       "}\n"
+       // D = 1: a lane owns 4 B; a chunk ends on 8 B, so its last 4 B are in range too
+       "__device__ static inline void ld1(u32 *e, unsigned long long p, long long o, long long C) {\n"
+       "  e[0] = o + 4 <= C ? __builtin_nontemporal_load(G1(p + o)) : 0u;\n"
+       "}\n"
+       "__device__ static inline void st1(const u32 *h, unsigned long long p, long long o, long long C) {\n"
+       "  if (o + 4 <= C) __builtin_nontemporal_store(h[0], GW1(p + o));\n"
+       "}\n"
+       "extern \"C\" __global__ __launch_bounds__(256) void lsec_xornet(Args a) {\n"
+       "  const long long C = a.size;\n"
+    << "  const unsigned tps = (unsigned)((C + " << tile - 1 << ") / " << tile << ");\n"
+    << "  const unsigned nt = tps * (unsigned)a.nstripes;\n"
+       "  const unsigned nb = gridDim.x, per = nb >> 3, rem = nb & 7, xcd = blockIdx.x & 7;\n"
+       "  const unsigned t0 = xcd * per + (xcd < rem ? xcd : rem) + (blockIdx.x >> 3);\n"
+       "  for (unsigned t = t0; t < nt; t += nb) {\n"
+       "    const unsigned s = t / tps;\n"
+    << "    const long long o0 = (long long)(t - s * tps) * " << tile << " + threadIdx.x * " << 4 * D << ";\n";
+  const int DL = D * IT;  // dwords per lane per shard
+  for (int j = 0; j < K; ++j) {
+    s << "    u32 e" << j << "[" << DL << "];\n    { const unsigned long long p = a.in[" << j << "].base + (unsigned long long)s * a.in["
+      << j << "].stride;\n";
+    for (int it = 0; it < IT; ++it)
+      s << "      ld" << D << "(e" << j << " + " << D * it << ", p, o0 + " << 256 * 4 * D * it << ", C);\n";
+    s << "    }\n";
+  }
+  for (size_t i = 0; i < pairs.size(); ++i)
+    s << "    u32 p" << i << "[" << DL << "];\n    for (int d = 0; d < " << DL << "; ++d) p" << i << "[d] = " << sym(pairs[i].first)
+      << " ^ " << sym(pairs[i].second) << ";\n";
+  for (int r = 0; r < R; ++r) {
+    s << "    { u32 h[" << DL << "];\n";
+    if (rows[r].empty()) s << "      for (int d = 0; d < " << DL << "; ++d) h[d] = 0u;\n";
+    // Horner over the coefficient bits: h = x(...x(S_top) + ...) + S_0
+    for (const Step &st : rows[r]) {
+      s << "      for (int d = 0; d < " << DL << "; ++d) {\n";
+      std::vector<std::string> terms;
+      if (st.doubled) {
+        s << "        const u32 x = XT(h[d]);\n";
+        terms.push_back("x");
+      }
+      for (int x : st.terms) terms.push_back(sym(x));
+      s << "        h[d] = " << xor_chain(terms) << ";\n      }\n";
+    }
+    s << "      const unsigned long long q = a.out[" << r << "].base + (unsigned long long)s * a.out[" << r << "].stride;\n";
+    for (int it = 0; it < IT; ++it) s << "      st" << D << "(h + " << D * it << ", q, o0 + " << 256 * 4 * D * it << ", C);\n";
+    s << "    }\n";
+  }
+  s << "  }\n}\n";
+  return s.str();
+}
+
+int xornet_tile(int K) {
+  int D = (jit_variant() >> 4) & 15;
+  if (D != 1 && D != 2 && D != 4) D = 4;
+  const int IT = D == 4 && K * 8 <= 104 ? 2 : 1;
+  return 256 * 4 * D * IT;
+}
+
+namespace {
+
+struct Entry {
+  std::vector<uint8_t> mat;
+  int R = 0, K = 0;
+  enum State { kCompiling, kReady, kFailed } state = kCompiling;
+  std::vector<char> code;                 // code object
+  std::map<int, hipModule_t> modules;     // device -> module
+  std::map<int, hipFunction_t> functions; // device -> kernel
+  std::string err;
+};
+
+std::mutex g_mu;
+std::condition_variable g_cv;
+std::map<std::vector<uint8_t>, std::shared_ptr<Entry>> g_by_matrix;  // key: R, K, matrix
+std::map<const void *, std::shared_ptr<Entry>> g_by_image;           // device image -> entry
+
+std::vector<uint8_t> key_of(const uint8_t *mat, int R, int K) {
+  std::vector<uint8_t> k(2 + static_cast<size_t>(R) * K);
+  k[0] = static_cast<uint8_t>(R);
+  k[1] = static_cast<uint8_t>(K);
+  std::memcpy(k.data() + 2, mat, static_cast<size_t>(R) * K);
+  return k;
+}
+
+void compile(std::shared_ptr<Entry> e) {
+  const std::string src = xornet_source(e->mat.data(), e->R, e->K);
+  hiprtcProgram prog = nullptr;
+  std::string err;
+  std::vector<char> code;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "lsec_xornet.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    err = "hiprtcCreateProgram failed";
+  } else {
+    const char *opts[] = {"--offload-arch=gfx950", "-O3"};
+    if (hiprtcCompileProgram(prog, 2, opts) != HIPRTC_SUCCESS) {
+      size_t n = 0;
+      hiprtcGetProgramLogSize(prog, &n);
+      std::string log(n, '\0');
+      if (n) hiprtcGetProgramLog(prog, &log[0]);
+      err = "hiprtc compile failed: " + log.substr(0, 400);
+    } else {
+      size_t n = 0;
+      hiprtcGetCodeSize(prog, &n);
+      code.resize(n);
+      hiprtcGetCode(prog, code.data());
+    }
+    hiprtcDestroyProgram(&prog);
+  }
+  static const bool trace = getenv("LSEC_TRACE") != nullptr;
+  if (trace || !err.empty())
+    fprintf(stderr, "[lsec jit] %dx%d xor network: %s\n", e->R, e->K, err.empty() ? "compiled" : err.c_str());
+  std::lock_guard<std::mutex> lk(g_mu);
+  e->code.swap(code);
+  e->err = err;
+  e->state = err.empty() ? Entry::kReady : Entry::kFailed;
+  g_cv.notify_all();
+}
+
+// the kernel of a ready entry on device `dev` (loads the module once per device; under g_mu)
+hipFunction_t function_locked(Entry &e, int dev) {
+  if (e.state != Entry::kReady) return nullptr;
+  auto it = e.functions.find(dev);
+  if (it != e.functions.end()) return it->second;
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr;
+  if (hipModuleLoadData(&mod, e.code.data()) != hipSuccess || hipModuleGetFunction(&fn, mod, "lsec_xornet") != hipSuccess) {
+    (void)hipGetLastError();
+    e.state = Entry::kFailed;
+    e.err = "module load failed";
+    return nullptr;
+  }
+  e.modules[dev] = mod;
+  e.functions[dev] = fn;
+  return fn;
+}
+
+}  // namespace
+
+void bind(const void *image, const uint8_t *mat, int R, int K) {
+  if (!image || !wants_xornet(R, K)) return;
+  std::shared_ptr<Entry> e;
+  bool start = false;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    const std::vector<uint8_t> key = key_of(mat, R, K);
+    auto it = g_by_matrix.find(key);
+    if (it == g_by_matrix.end()) {
+      e = std::make_shared<Entry>();
+      e->mat.assign(mat, mat + static_cast<size_t>(R) * K);
+      e->R = R;
+      e->K = K;
+      g_by_matrix.emplace(key, e);
+      start = true;
+    } else {
+      e = it->second;
+    }
+    g_by_image[image] = e;
+  }
+  if (start) std::thread(compile, e).detach();
+}
+
+void unbind(const void *image) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_by_image.erase(image);
+}
+
+int wait(const void *image, int timeout_ms) {
+  std::unique_lock<std::mutex> lk(g_mu);
+  auto it = g_by_image.find(image);
+  if (it == g_by_image.end()) return 0;
+  std::shared_ptr<Entry> e = it->second;
+  g_cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return e->state != Entry::kCompiling; });
+  return e->state == Entry::kReady ? 1 : 0;
+}
+
+hipFunction_t ready(const void *image, int R, int K) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_by_image.find(image);
+  if (it == g_by_image.end() || it->second->R != R || it->second->K != K) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  return function_locked(*it->second, dev);
+}
+
+hipError_t launch(hipFunction_t fn, int R, int K, const ShardRef *in, const ShardRef *out, int nstripes, int64_t size,
+                  hipStream_t st) {
+  // struct Args { long long size; int nstripes; int pad; Ref in[K]; Ref out[R]; }
+  std::vector<uint8_t> args(16 + sizeof(ShardRef) * (K + R));
+  std::memcpy(args.data(), &size, 8);
+  std::memcpy(args.data() + 8, &nstripes, 4);
+  std::memcpy(args.data() + 16, in, sizeof(ShardRef) * K);
+  std::memcpy(args.data() + 16 + sizeof(ShardRef) * K, out, sizeof(ShardRef) * R);
+  size_t bytes = args.size();
+  void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes, HIP_LAUNCH_PARAM_END};
+  const int64_t tile = xornet_tile(K);  // as xornet_source
+  const uint64_t ntiles = static_cast<uint64_t>((size + tile - 1) / tile) * static_cast<uint64_t>(nstripes);
+  if (ntiles == 0) return hipSuccess;
+  if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
+  return hipModuleLaunchKernel(fn, static_cast<unsigned>(ntiles), 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+}
+
+}  // namespace jit
+}  // namespace lsec

@@ -1,0 +1,40 @@
+// ec_jit.h -- run-time compiled XOR networks for wide GF(2^8) matrix codes (ec_jit.cpp).
+// Internal to liblstore_ec.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "ec_kernels.h"
+
+namespace lsec {
+namespace jit {
+
+constexpr int kMaxRows = 8;   // output rows one network computes
+constexpr int kMaxCols = 32;  // input columns (registers: 8 slices per input per lane)
+
+// whether an R x K bytewise matrix is served by a network (wide codes only; LSEC_JIT=0: never)
+bool wants_xornet(int R, int K);
+// HIP source of the network for the row-major R x K matrix (exposed for tests and tools)
+std::string xornet_source(const uint8_t *mat, int R, int K);
+// bytes of a shard one 256-lane block of the network covers per tile
+int xornet_tile(int K);
+// LSEC_JIT_VARIANT (code shape knobs for A/B runs; 0 = default)
+int jit_variant();
+// Associate a device coefficient image with its matrix and start compiling that matrix's
+// network in the background (once per matrix per process).  unbind before the image is freed.
+void bind(const void *image, const uint8_t *mat, int R, int K);
+void unbind(const void *image);
+// Block until the image's network is compiled (or failed, or timeout): 1 ready, 0 otherwise
+// (also 0 when the image has no network).
+int wait(const void *image, int timeout_ms);
+// The compiled network for `image` on the current device, or nullptr (not bound / not ready).
+hipFunction_t ready(const void *image, int R, int K);
+// out[r] = sum_j A[r][j] in[j] for every stripe (same shard addressing as ApplyArgs).
+hipError_t launch(hipFunction_t fn, int R, int K, const ShardRef *in, const ShardRef *out, int nstripes, int64_t size,
+                  hipStream_t st);
+
+}  // namespace jit
+}  // namespace lsec

@@ -152,5 +152,6 @@ void make_word_cell(uint32_t c, int w, uint32_t *out);
 
 // Variant selection knobs for experiments: 0 = default
 void set_kernel_variant(int bytewise_variant, int bitsliced_variant);
+int bytewise_variant();  // != 0: a forced bytewise shape (also keeps wide codes off their XOR networks)
 
 }  // namespace lsec

@@ -57,6 +57,8 @@ void set_kernel_variant(int bw, int bs) {
   g_bs_variant = bs;
 }
 
+int bytewise_variant() { return g_bw_variant; }
+
 hipError_t launch_bytewise(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
   if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > 8 || a.size % 8 != 0) return hipErrorInvalidValue;
   if (a.nstripes <= 0 || a.size == 0) return hipSuccess;

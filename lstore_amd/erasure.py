@@ -73,7 +73,7 @@ EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan",
            "lsec_decode_dev", "et_encode_stripes_magic", "et_stripes_magic", "lsec_encode_magic_dev",
            "lsec_stripe_magic_dev", "lsec_segment_write", "lsec_segment_read", "lsec_segment_inspect",
            "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count", "lsec_last_error", "lsec_plan_kernel",
-           "lsec_set_kernel_variant", "lsec_set_host_devices", "lsec_hbm_copy_dev")
+           "lsec_set_kernel_variant", "lsec_set_host_devices", "lsec_hbm_copy_dev", "lsec_prepare_encode", "lsec_plan_jit")
 
 # read / inspect flags and stripe states (include/lstore_ec.h)
 READ_PARANOID, MAGIC_LEGACY, INSPECT_FIX, MAX_DEVS = 1, 2, 4, 64
@@ -127,6 +127,8 @@ def lib():
     L.lsec_encode_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.c_void_p]
     L.lsec_decode_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.POINTER(C.c_int), C.c_void_p]
     L.lsec_prepare_decode.argtypes = [P, C.POINTER(C.c_int)]
+    L.lsec_prepare_encode.argtypes = [P]
+    L.lsec_plan_jit.argtypes = [P, C.POINTER(C.c_int)]
     L.et_encode_stripes_magic.argtypes = [P, C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_void_p]
     L.et_stripes_magic.argtypes = [P, C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_void_p]
     L.lsec_encode_magic_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.c_void_p, C.c_void_p]
@@ -419,6 +421,14 @@ class Plan:
 
     def prepare_decode(self, erasures) -> None:
         _check(lib().lsec_prepare_decode(self._p, _erasure_array(erasures)), "lsec_prepare_decode")
+
+    def prepare_encode(self) -> None:
+        """Build the encode image on the current device and wait for a wide code's XOR network."""
+        _check(lib().lsec_prepare_encode(self._p), "lsec_prepare_encode")
+
+    def jit(self, erasures=None) -> bool:
+        """True when the encode (or the decode of `erasures`) runs on a compiled XOR network."""
+        return bool(lib().lsec_plan_jit(self._p, None if erasures is None else _erasure_array(erasures)))
 
 
 def _stream_handle(stream) -> int:

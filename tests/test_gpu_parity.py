@@ -329,6 +329,42 @@ def test_wide_stripes_vs_oracle(cuda, method, k, m, size):
             assert np.array_equal(st, full), pat
 
 
+@pytest.mark.parametrize("k,m,size", [
+    (20, 6, 65536),          # RS(20+6): the c5 wide code, whole 16 B lanes
+    (20, 6, 4096 * 3 + 24),  # ragged: the last lane's 16 B piece is 8 B
+    (16, 6, 40968),          # R * K = 96: the smallest matrix served by a network
+    (32, 8, 8192),           # the widest network (K = 32, R = 8)
+])
+def test_xor_network_vs_oracle(cuda, k, m, size):
+    """Wide RS codes run on their compiled XOR networks (ec_jit.cpp) once prepared: encode and
+    an m-device decode (R = m rows over K = k survivors) bit-exact vs the oracle, device-resident
+    and from host memory."""
+    import torch
+    n = 3
+    rng = np.random.default_rng(k * 100 + m)
+    st = np.zeros((n, k + m, size), dtype=np.uint8)
+    st[:, :k] = rng.integers(0, 256, (n, k, size), dtype=np.uint8)
+    st[1, :k] = 0xFF  # every bit set: every Horner step's doubling reduces
+    lost = list(range(m))  # data shards 0..m-1: the decode matrix is dense
+    with L.Plan.new(L.REED_SOL_VAN, size, k, m, 8, 8, 8) as p:
+        assert p.form_encoding_matrix() == 0 and p.form_decoding_matrix() == 0
+        p.prepare_encode()
+        p.prepare_decode(lost)
+        assert p.jit() == 1 and p.jit(lost) == 1, "network not compiled"
+        want = np.stack([O.encode(L.REED_SOL_VAN, st[s, :k], m, 0) for s in range(n)])
+        data = torch.from_numpy(st[:, :k].copy()).cuda()
+        par = torch.full((n, m, size), 0x5A, dtype=torch.uint8, device="cuda")
+        p.encode_dev(data, par)
+        assert np.array_equal(par.cpu().numpy(), want)
+        host = st.copy()
+        p.encode_stripes(host)
+        assert np.array_equal(host[:, k:], want)
+        full = host.copy()
+        host[:, lost] = 0x33
+        p.decode_stripes(host, lost)
+        assert np.array_equal(host, full)
+
+
 def test_stripe_width_limits_are_errors(cuda):
     """m > 64 (LSEC_MAX_DEVS) is refused with a message, never written past a table."""
     k, m, size = 4, 65, 4096

@@ -57,6 +57,8 @@ def main():
         data = torch.randint(0, 256, (N, k, C + a.pad), dtype=torch.uint8, device=dev)[:, :, :C]
         par = torch.empty((N, m, C + a.pad), dtype=torch.uint8, device=dev)[:, :, :C]
         out = torch.empty((N, 1, C), dtype=torch.uint8, device=dev)
+        plan.prepare_encode()  # wide codes: wait for the compiled XOR network (variant 0,0 uses it)
+        plan.prepare_decode([0])
         plan.encode_dev(data, par)
         ref_par = par.clone()
         stream = torch.cuda.current_stream()
@@ -83,7 +85,7 @@ def main():
             td = sorted(res[v][1])[len(res[v][1]) // 2]
             eb = (k + m) * C * N
             db = (k + 1) * C * N
-            print(f"{name:6s} N={N:5d} variant={v}  encode {te:8.3f} ms {eb / te / 1e6:7.1f} GB/s "
+            print(f"{name:6s} N={N:5d} variant={v} jit={int(plan.jit()) if v == (0, 0) else 0}  encode {te:8.3f} ms {eb / te / 1e6:7.1f} GB/s "
                   f"({eb / te / 8e9:5.1%})   decode {td:8.3f} ms {db / td / 1e6:7.1f} GB/s ({db / td / 8e9:5.1%})",
                   flush=True)
         E.set_kernel_variant(0, 0)

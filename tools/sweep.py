@@ -54,6 +54,8 @@ def main():
         for k, m in km:
             for C in chunks:
                 plan = L.Plan.for_chunk(meth, k, m, C)
+                plan.prepare_encode()
+                plan.prepare_decode([0])
                 N = max(2, int(a.dev_gib * 2**30 / (k * C)))
                 data = torch.randint(0, 256, (N, k, C), dtype=torch.uint8, device=dev)
                 par = torch.empty((N, m, C), dtype=torch.uint8, device=dev)
@@ -96,6 +98,7 @@ def main():
                 gib_d, gib_h = k * C * N / 2**30, k * C * Nh / 2**30
                 rec = {"config": "c5", "rank": rank, "method": mname, "k": k, "m": m, "chunk": C,
                        "packet": plan.packet_size, "kernel": "bytewise" if plan.kernel == 1 else "bitsliced",
+                       "jit_encode": plan.jit(), "jit_decode": plan.jit([0]),
                        "dev_stripes": N, "enc_gibps": round(gib_d / te, 1), "dec_gibps": round(gib_d / td, 1),
                        "enc_hbm_frac": round((k + m) * C * N / te / 8e12, 4),
                        "dec_hbm_frac": round((k + 1) * C * N / td / 8e12, 4),
