@@ -93,7 +93,7 @@ int et_decode(lio_erasure_plan_t *plan, long long int fsize, const char *fname, 
 
 /* ===================================================================== Part 2: extensions */
 
-#define LSEC_ABI_VERSION 1
+#define LSEC_ABI_VERSION 2
 
 /* Stripe-batched host-memory calls.  ptrs holds nstripes*(k+m) pointers laid out exactly
  * like segjerase_write_func's ptr[] array (segment/jerasure.c:1647, :1812-1836): stripe s
@@ -139,13 +139,23 @@ int lsec_stripe_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, 
  * Parity and magics are computed on the GPU.  0 / -1. */
 int lsec_segment_write(lio_erasure_plan_t *plan, const char *data, int nstripes, int chunk, int n_shift,
                        long long first_stripe, char **dev);
+/* The same with the user data as a scatter list (the tbuf's iovecs, segment/jerasure.c:1786-1825):
+ * stripe s covers bytes [s*k*C, (s+1)*k*C) of the concatenated pieces.  A stripe inside one
+ * piece is read in place; a stripe straddling pieces is gathered into a contiguous copy first
+ * (:1795-1811); a stripe whose first piece is an error page (iov_base NULL) is encoded and
+ * written as zero data chunks (:1816, :1823-1831).  Error pages inside a straddling stripe read
+ * as zeros (the reference would read through the NULL base).  0 / -1 (fewer than nstripes*k*C
+ * bytes listed is an error). */
+struct iovec;
+int lsec_segment_write_iov(lio_erasure_plan_t *plan, const struct iovec *iov, int n_iov, int nstripes, int chunk,
+                           int n_shift, long long first_stripe, char **dev);
 
 /* Flags of the read / inspect entry points */
 #define LSEC_READ_PARANOID 1   /* verify every stripe, not only those with bad chunks */
 #define LSEC_MAGIC_LEGACY  2   /* segment magic_cksum == 0: magics are not adler32 sums, so
                                   stripes are verified with control chunks (jerasure.c:218-266) */
 #define LSEC_INSPECT_FIX   4   /* inspect: repair in place (INSPECT_{QUICK,SCAN,FULL}_REPAIR) */
-#define LSEC_MAX_DEVS      64
+#define LSEC_MAX_DEVS      256
 
 /* Batched read side for whole stripes (segjerase_read_func, segment/jerasure.c:1255-1631):
  * dev[i] are device images laid out as lsec_segment_write writes them (NULL = device

@@ -67,7 +67,10 @@ int fail(const char *fmt, ...) {
 
 enum KernelKind { KNONE = 0, KBYTEWISE = 1, KBITSLICED = 2, KBITMATRIX = 3, KWORDWISE = 4, KBITSLICEDW = 5 };
 
-constexpr int kMaxM = 64;  // parity devices per stripe (output shard tables below are sized for it)
+// devices per stripe: Jerasure takes k + m <= 2^w (reed_sol.c:247-248, cauchy.c:139), 256 at w = 8;
+// the engine takes k + m <= 256 at every w (LSEC_MAX_DEVS).  Inputs beyond lsec::kMaxK per launch
+// run as several launches over the grouped image layout (ec_kernels.h).
+constexpr int kMaxDevs = LSEC_MAX_DEVS;
 
 struct DecodeEntry {
   lsec::gf8::DecodePlan dp;
@@ -111,7 +114,7 @@ bool liberation_family(int method) { return method == BLAUM_ROTH || method == LI
 //   Cauchy at w = 8 -> bit-sliced GF(2^8); at w = 16 / 32 -> bit-sliced GF(2^w)
 //   liberation family -> generic GF(2) bitmatrix; raid4 -> bytewise XOR (w unused, raid4.c)
 int kernel_kind(int method, int w) {
-  if (liberation_family(method)) return lsec::bitmatrix_w_supported(w) ? KBITMATRIX : KNONE;
+  if (liberation_family(method)) return w >= 2 && w <= lsec::kMaxW ? KBITMATRIX : KNONE;
   if (method == RAID4) return KBYTEWISE;
   const bool wide = (w == 16 || w == 32);
   if (w != 8 && !wide) return KNONE;
@@ -143,14 +146,41 @@ std::vector<uint32_t> word_image(const lsec::gfw::Mat &mat, int rows, int cols, 
   return img;
 }
 
-// bitmatrix row masks for the generic bitmatrix kernel: word [(r*w+l)*k + j], bit x = B[r*w+l][j*w+x]
+// bitmatrix row masks for the generic bitmatrix kernels: NW = mask_words(w) words per (row, input),
+// bit x of word [((r*w+l)*k + j)*NW + q] = B[r*w+l][j*w + 32q + x]
 std::vector<uint32_t> bitmatrix_masks(const int *bm, int k, int m, int w) {
-  std::vector<uint32_t> mk(static_cast<size_t>(m) * w * k, 0u);
+  const int nw = lsec::mask_words(w);
+  std::vector<uint32_t> mk(static_cast<size_t>(m) * w * k * nw, 0u);
   for (int row = 0; row < m * w; ++row)
     for (int j = 0; j < k; ++j)
       for (int x = 0; x < w; ++x)
-        if (bm[static_cast<size_t>(row) * k * w + j * w + x]) mk[static_cast<size_t>(row) * k + j] |= 1u << x;
+        if (bm[static_cast<size_t>(row) * k * w + j * w + x])
+          mk[(static_cast<size_t>(row) * k + j) * nw + x / 32] |= 1u << (x % 32);
   return mk;
+}
+
+// Image rows per output row and elements per (row, input) of a kernel kind's image.
+int image_rows_per_output(int kind, int w) { return kind == KBITMATRIX ? w : 1; }
+int image_unit(int kind, int w) {
+  return kind == KBITMATRIX ? lsec::mask_words(w) : (kind == KWORDWISE || kind == KBITSLICEDW) ? w : 1;
+}
+
+// The grouped layout of ec_kernels.h for images of more than lsec::kMaxK inputs: `rows` image
+// rows of K inputs x `unit` elements, row-major -> groups of kMaxK inputs, each row-major.
+template <typename T>
+void group_image(std::vector<T> &img, int rows, int K, int unit) {
+  if (K <= lsec::kMaxK) return;
+  std::vector<T> out(img.size());
+  size_t o = 0;
+  for (int k0 = 0; k0 < K; k0 += lsec::kMaxK) {
+    const int kg = std::min(lsec::kMaxK, K - k0);
+    for (int r = 0; r < rows; ++r) {
+      const T *src = &img[(static_cast<size_t>(r) * K + k0) * unit];
+      std::copy(src, src + static_cast<size_t>(kg) * unit, &out[o]);
+      o += static_cast<size_t>(kg) * unit;
+    }
+  }
+  img.swap(out);
 }
 
 int *to_int_array(const lsec::gf8::Mat &m) {
@@ -256,6 +286,7 @@ int form_matrices(lio_erasure_plan_t *p, bool with_schedule) {
   if (kind == KBITMATRIX) {
     if (!p->encode_bitmatrix) return 0;
     e->impl->enc_masks = bitmatrix_masks(p->encode_bitmatrix, k, m, w);
+    group_image(e->impl->enc_masks, m * w, k, lsec::mask_words(w));
     e->impl->coding_ready = true;
   } else if (p->encode_matrix) {
     const int rows = (p->method == REED_SOL_R6_OP) ? 2 : m;
@@ -263,6 +294,7 @@ int form_matrices(lio_erasure_plan_t *p, bool with_schedule) {
       e->impl->coding_w.resize(static_cast<size_t>(rows) * k);
       for (size_t i = 0; i < e->impl->coding_w.size(); ++i) e->impl->coding_w[i] = static_cast<uint32_t>(p->encode_matrix[i]);
       e->impl->enc_masks = word_image(e->impl->coding_w, rows, k, w);
+      group_image(e->impl->enc_masks, rows, k, w);
     } else {
       e->impl->coding.resize(static_cast<size_t>(rows) * k);
       for (size_t i = 0; i < e->impl->coding.size(); ++i) e->impl->coding[i] = static_cast<uint8_t>(p->encode_matrix[i]);
@@ -369,6 +401,7 @@ int encode_cells(PlanExt *e, const void **out) {
   const int rows = static_cast<int>(e->impl->coding.size()) / k;
   std::vector<CoefCell> h;
   host_cells(e->impl->coding, rows, k, h);
+  group_image(h, rows, k, 1);
   CoefCell *d = nullptr;
   if (upload_cells(h, &d)) return -1;
   e->impl->enc_cells[dev] = d;
@@ -419,6 +452,7 @@ int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, con
       ent.dp.survivors = wp.survivors;
       ent.dp.erased = wp.erased;
       ent.masks = word_image(wp.rows, static_cast<int>(wp.erased.size()), k, w);
+      group_image(ent.masks, static_cast<int>(wp.erased.size()), k, w);
       ent.xor_only = std::all_of(wp.rows.begin(), wp.rows.end(), [](uint32_t c) { return c <= 1u; });
       if (ent.xor_only) ent.dp.rows.assign(wp.rows.begin(), wp.rows.end());  // 0 / 1 as GF(2^8) cells
     } else if (kind == KBITMATRIX) {
@@ -426,6 +460,7 @@ int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, con
       std::vector<int> bm(p->encode_bitmatrix, p->encode_bitmatrix + static_cast<size_t>(k) * p->parity_strips * p->w * p->w);
       if (!lsec::gf8::make_bit_decode(k, p->parity_strips, p->w, bm, ids, ent.dp, ent.masks))
         return fail("decoding bitmatrix is singular");
+      group_image(ent.masks, static_cast<int>(ent.dp.erased.size()) * p->w, k, lsec::mask_words(p->w));
     } else {
       const int m = static_cast<int>(e->impl->coding.size()) / k;
       if (!lsec::gf8::make_decode(k, m, e->impl->coding, ids, ent.dp)) return fail("decoding matrix is singular");
@@ -449,6 +484,7 @@ int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, con
   if (dc == ent.dev_cells.end()) {
     std::vector<CoefCell> h;
     host_cells(ent.dp.rows, static_cast<int>(ent.dp.erased.size()), e->pub.data_strips, h);
+    group_image(h, static_cast<int>(ent.dp.erased.size()), e->pub.data_strips, 1);
     CoefCell *d = nullptr;
     if (upload_cells(h, &d)) return -1;
     dc = ent.dev_cells.emplace(dev, d).first;
@@ -471,8 +507,7 @@ int decode_kind(const PlanExt *e, const DecodeEntry *ent) {
 
 int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
   const int k = p->data_strips, m = p->parity_strips;
-  if (k < 1 || k > lsec::kMaxK) return fail("k=%d outside 1..%d", k, lsec::kMaxK);
-  if (m < 1 || m > kMaxM) return fail("m=%d outside 1..%d", m, kMaxM);
+  if (k < 1 || m < 1 || k + m > kMaxDevs) return fail("k=%d m=%d: k+m outside 2..%d", k, m, kMaxDevs);
   if (block_size < 0 || block_size % 8 != 0) return fail("block_size %lld is not a multiple of 8", block_size);
   const int kind = kernel_kind(p->method, p->w);
   if (kind == KNONE)
@@ -487,8 +522,9 @@ int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
 }
 
 // Enqueue out[r] = rows[r] . in  for every stripe, splitting R into launches of <= 8 rows
-// (<= 2 for the bitmatrix kernel).  `image` is the CoefCell[R][K] matrix image, or for
-// KBITMATRIX the uint32 row masks [(r*w+l)*K + j].
+// (<= 2 for the bitmatrix kernel) and K into groups of <= lsec::kMaxK inputs.  `image` is the
+// CoefCell[R][K] matrix image, the uint32 row masks [((r*w+l)*K + j)*NW + q] (KBITMATRIX) or the
+// word products [(r*K + j)*w + b] (KWORDWISE / KBITSLICEDW), grouped when K > kMaxK.
 int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in, const ShardRef *out,
                   int nstripes, long long size, int packet, hipStream_t st, int w = 8) {
   if (kind == KBYTEWISE && lsec::bytewise_variant() == 0 && lsec::jit::wants_xornet(R, K)) {
@@ -507,35 +543,43 @@ int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in,
     }
   }
   const int rmax = kind == KBITMATRIX ? 2 : ((kind == KBITSLICEDW || kind == KWORDWISE) && w == 32) ? 4 : 8;
-  for (int r0 = 0; r0 < R; r0 += rmax) {
-    lsec::ApplyArgs a;
-    std::memset(&a, 0, sizeof(a));
-    a.K = K;
-    a.R = std::min(rmax, R - r0);
-    if (uses_u32_image(kind)) {  // both images hold w words per (row, input) in row-major order
-      a.masks = static_cast<const uint32_t *>(image) + static_cast<size_t>(r0) * w * K;
-      a.w = w;
-    } else {
-      a.cells = static_cast<const CoefCell *>(image) + static_cast<size_t>(r0) * K;
-    }
-    a.nstripes = nstripes;
-    a.size = size;
-    a.packet = packet;
-    for (int j = 0; j < K; ++j) a.in[j] = in[j];
-    for (int r = 0; r < a.R; ++r) a.out[r] = out[r0 + r];
-    // split very large batches so tile indices stay 32-bit
-    const long long per = std::max(1LL, (1LL << 30) / std::max(1LL, size / 4096 + 1));
-    for (int s0 = 0; s0 < nstripes; s0 += static_cast<int>(std::min<long long>(per, nstripes))) {
-      lsec::ApplyArgs b = a;
-      b.nstripes = static_cast<int>(std::min<long long>(per, nstripes - s0));
-      for (int j = 0; j < K; ++j) b.in[j].base = in[j].base + static_cast<uint64_t>(s0) * in[j].stride;
-      for (int r = 0; r < b.R; ++r) b.out[r].base = out[r0 + r].base + static_cast<uint64_t>(s0) * out[r0 + r].stride;
-      const hipError_t err = kind == KBYTEWISE    ? lsec::launch_bytewise(b, st)
-                             : kind == KBITMATRIX ? lsec::launch_bitmatrix(b, st)
-                             : kind == KWORDWISE  ? lsec::launch_wordwise(b, st)
-                             : kind == KBITSLICEDW ? lsec::launch_gfw_bitsliced(b, st)
-                                                  : lsec::launch_bitsliced(b, st);
-      if (err != hipSuccess) return fail("kernel launch failed: %s", hipGetErrorString(err));
+  const int rpr = image_rows_per_output(kind, w), unit = image_unit(kind, w);
+  // input groups of at most kMaxK (grouped image layout); groups after the first accumulate
+  for (int k0 = 0; k0 < K; k0 += lsec::kMaxK) {
+    const int kg = std::min(lsec::kMaxK, K - k0);
+    const size_t group_base = static_cast<size_t>(k0) * R * rpr * unit;  // earlier groups: kMaxK inputs each
+    for (int r0 = 0; r0 < R; r0 += rmax) {
+      lsec::ApplyArgs a;
+      std::memset(&a, 0, sizeof(a));
+      a.K = kg;
+      a.R = std::min(rmax, R - r0);
+      a.accumulate = k0 > 0;
+      const size_t at = group_base + static_cast<size_t>(r0) * rpr * kg * unit;
+      if (uses_u32_image(kind)) {  // w words per (row, input), or mask words per (bit-row, input)
+        a.masks = static_cast<const uint32_t *>(image) + at;
+        a.w = w;
+      } else {
+        a.cells = static_cast<const CoefCell *>(image) + at;
+      }
+      a.nstripes = nstripes;
+      a.size = size;
+      a.packet = packet;
+      for (int j = 0; j < kg; ++j) a.in[j] = in[k0 + j];
+      for (int r = 0; r < a.R; ++r) a.out[r] = out[r0 + r];
+      // split very large batches so tile indices stay 32-bit
+      const long long per = std::max(1LL, (1LL << 30) / std::max(1LL, size / 4096 + 1));
+      for (int s0 = 0; s0 < nstripes; s0 += static_cast<int>(std::min<long long>(per, nstripes))) {
+        lsec::ApplyArgs b = a;
+        b.nstripes = static_cast<int>(std::min<long long>(per, nstripes - s0));
+        for (int j = 0; j < kg; ++j) b.in[j].base = in[k0 + j].base + static_cast<uint64_t>(s0) * in[k0 + j].stride;
+        for (int r = 0; r < b.R; ++r) b.out[r].base = out[r0 + r].base + static_cast<uint64_t>(s0) * out[r0 + r].stride;
+        const hipError_t err = kind == KBYTEWISE    ? lsec::launch_bytewise(b, st)
+                               : kind == KBITMATRIX ? lsec::launch_bitmatrix(b, st)
+                               : kind == KWORDWISE  ? lsec::launch_wordwise(b, st)
+                               : kind == KBITSLICEDW ? lsec::launch_gfw_bitsliced(b, st)
+                                                    : lsec::launch_bitsliced(b, st);
+        if (err != hipSuccess) return fail("kernel launch failed: %s", hipGetErrorString(err));
+      }
     }
   }
   return 0;
@@ -550,7 +594,7 @@ int encode_dev(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C, hi
   if (encode_cells(e, &cells)) return -1;
   const int k = p->data_strips;
   const int R = encode_rows(e);  // m (2 for r6, 1 for raid4)
-  ShardRef in[lsec::kMaxK], out[kMaxM];
+  ShardRef in[kMaxDevs], out[kMaxDevs];
   for (int j = 0; j < k; ++j) in[j] = {reinterpret_cast<uint64_t>(sh[j].base), sh[j].stride};
   for (int r = 0; r < R; ++r) out[r] = {reinterpret_cast<uint64_t>(sh[k + r].base), sh[k + r].stride};
   return enqueue_apply(kernel_kind(p->method, p->w), cells, k, R, in, out, nstripes, C, p->packet_size, st, p->w);
@@ -571,7 +615,7 @@ int decode_dev(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C, co
   const void *cells = nullptr;
   if (decode_entry(e, ids, &ent, &cells)) return -1;
   const int k = p->data_strips;
-  ShardRef in[lsec::kMaxK], out[kMaxM];
+  ShardRef in[kMaxDevs], out[kMaxDevs];
   for (int j = 0; j < k; ++j) {
     const lsec_shard_t &s = sh[ent->dp.survivors[j]];
     in[j] = {reinterpret_cast<uint64_t>(s.base), s.stride};
@@ -1085,6 +1129,20 @@ hipError_t issue_runs(const std::vector<DmaRun> &v, hipMemcpyKind kind, hipStrea
   return hipSuccess;
 }
 
+// Stripe magic partial sums over `km` shards in checksum order (sh[i] = shard i), in launches
+// of at most kMaxMagicShards shards; `ma` carries everything else.
+hipError_t launch_magic_groups(lsec::MagicArgs ma, const ShardRef *sh, int km, hipStream_t st) {
+  ma.total_shards = km;
+  for (int i0 = 0; i0 < km; i0 += lsec::kMaxMagicShards) {
+    ma.shard0 = i0;
+    ma.nshards = std::min(lsec::kMaxMagicShards, km - i0);
+    for (int i = 0; i < ma.nshards; ++i) ma.sh[i] = sh[i0 + i];
+    const hipError_t err = lsec::launch_stripe_magic(ma, st);
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
+}
+
 // Shared driver of the host-memory paths.  For each stripe, `in_ids` name the shards that
 // go to the GPU and `out_ids` the shards that come back (encode: data -> parity; decode:
 // survivors -> erased).  The kernel runs on the packed staging layout.
@@ -1102,7 +1160,6 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   for (size_t j = 0; j < in_ids.size(); ++j) where[in_ids[j]] = static_cast<int>(j);
   for (size_t r = 0; r < out_ids.size(); ++r) where[out_ids[r]] = -2 - static_cast<int>(r);
   if (magic_host) {
-    if (km > lsec::kMaxMagicShards) return fail("stripe magic supports at most %d chunks", lsec::kMaxMagicShards);
     for (int i = 0; i < km; ++i)
       if (where[i] == -1) return fail("stripe magic needs all %d chunks staged", km);
   }
@@ -1245,7 +1302,7 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
       if (err == hipSuccess) err = hipEventRecord(sl.in_done, stg->s_in);
       if (err == hipSuccess) err = hipStreamWaitEvent(stg->s_out, sl.in_done, 0);
       if (err != hipSuccess) { rc = fail("H2D: %s", hipGetErrorString(err)); break; }
-      ShardRef in[lsec::kMaxK], out[kMaxM];
+      ShardRef in[kMaxDevs], out[kMaxDevs];
       for (int j = 0; j < nin; ++j)
         in[j] = {reinterpret_cast<uint64_t>(sl.d) + static_cast<uint64_t>(j) * len, static_cast<int64_t>(nin * len)};
       for (int r = 0; r < nout; ++r)
@@ -1254,14 +1311,14 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
       if (magic_host) {
         lsec::MagicArgs ma;
         std::memset(&ma, 0, sizeof(ma));
-        ma.nshards = km;
         ma.nstripes = nb;
         ma.size = clen;
         ma.col0 = c0;
         ma.chunk = C;
         ma.acc = dacc + 2ull * s0;
-        for (int i = 0; i < km; ++i) ma.sh[i] = where[i] >= 0 ? in[where[i]] : out[-2 - where[i]];
-        err = lsec::launch_stripe_magic(ma, stg->s_out);
+        ShardRef msh[kMaxDevs];
+        for (int i = 0; i < km; ++i) msh[i] = where[i] >= 0 ? in[where[i]] : out[-2 - where[i]];
+        err = launch_magic_groups(ma, msh, km, stg->s_out);
         if (err != hipSuccess) { rc = fail("magic launch: %s", hipGetErrorString(err)); break; }
       }
       if (nout > 0 && out_by_kernel) {
@@ -1612,7 +1669,7 @@ class Dispatcher {
       const int nin = static_cast<int>(r0.in_ids.size()), nout = static_cast<int>(r0.out_ids.size());
       const size_t in_bytes = static_cast<size_t>(g.nstripes) * nin * C;
       char *dbase = sl.d + g.off;
-      ShardRef in[lsec::kMaxK], out[kMaxM];
+      ShardRef in[kMaxDevs], out[kMaxDevs];
       for (int j = 0; j < nin; ++j)
         in[j] = {reinterpret_cast<uint64_t>(dbase) + static_cast<uint64_t>(j) * C, static_cast<int64_t>(nin * C)};
       for (int o = 0; o < nout; ++o)
@@ -2066,7 +2123,7 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
   const lio_erasure_plan_t *p = &e->pub;
   const int km = p->data_strips + p->parity_strips;
   const size_t nin = in_ids.size(), nout = out_ids.size(), nio = nin + nout;
-  ShardRef in[lsec::kMaxK], out[kMaxM];
+  ShardRef in[kMaxDevs], out[kMaxDevs];
   const bool aligned = kernel_transport_aligned(ptrs, nstripes, km, in_ids, out_ids, C, C);
   static thread_local std::map<int, std::unique_ptr<ZcSlot>> slots;
   std::unique_ptr<ZcSlot> &slot = slots[dev];
@@ -2167,7 +2224,7 @@ int run_direct(PlanExt *e, char **ptrs, long long C, const std::vector<int> &in_
   }
   hipStream_t st = thread_stream();
   if (!st) return fail("no HIP stream");
-  ShardRef in[lsec::kMaxK], out[kMaxM];
+  ShardRef in[kMaxDevs], out[kMaxDevs];
   for (size_t j = 0; j < nin; ++j) {
     HIP_OK(hipMemcpyAsync(sc.d + j * C, ptrs[in_ids[j]], C, hipMemcpyHostToDevice, st));
     in[j] = {reinterpret_cast<uint64_t>(sc.d) + j * C, 0};
@@ -2332,7 +2389,7 @@ int stripes_magic_impl(PlanExt *e, char **ptrs, int nstripes, long long C, uint8
 int magic_dev_impl(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C, uint8_t *magic, hipStream_t st) {
   lio_erasure_plan_t *p = &e->pub;
   const int km = p->data_strips + p->parity_strips;
-  if (km > lsec::kMaxMagicShards) return fail("stripe magic supports at most %d chunks", lsec::kMaxMagicShards);
+  if (km > kMaxDevs) return fail("stripe magic supports at most %d chunks", kMaxDevs);
   if (C < 0 || C % 8 != 0) return fail("block_size %lld is not a multiple of 8", C);
   if (nstripes <= 0 || C == 0) return 0;
   unsigned long long *acc = nullptr;
@@ -2340,17 +2397,17 @@ int magic_dev_impl(PlanExt *e, const lsec_shard_t *sh, int nstripes, long long C
   HIP_OK(hipMemsetAsync(acc, 0, 16ull * nstripes, st));
   lsec::MagicArgs ma;
   std::memset(&ma, 0, sizeof(ma));
-  ma.nshards = km;
   ma.size = C;
   ma.col0 = 0;
   ma.chunk = C;
   const int per = static_cast<int>(std::max(1LL, (1LL << 30) / std::max(1LL, C / 8192 + 1)));
+  ShardRef msh[kMaxDevs];
   for (int s0 = 0; s0 < nstripes; s0 += per) {
     ma.nstripes = std::min(per, nstripes - s0);
     ma.acc = acc + 2ull * s0;
     for (int i = 0; i < km; ++i)
-      ma.sh[i] = {reinterpret_cast<uint64_t>(sh[i].base) + static_cast<uint64_t>(s0) * sh[i].stride, sh[i].stride};
-    HIP_OK(lsec::launch_stripe_magic(ma, st));
+      msh[i] = {reinterpret_cast<uint64_t>(sh[i].base) + static_cast<uint64_t>(s0) * sh[i].stride, sh[i].stride};
+    HIP_OK(launch_magic_groups(ma, msh, km, st));
   }
   HIP_OK(lsec::launch_magic_finalize(acc, nstripes, static_cast<int64_t>(km) * C, magic, st));
   HIP_OK(hipFreeAsync(acc, st));
@@ -2848,8 +2905,8 @@ lio_erasure_plan_t *et_generate_plan(long long int file_size, int method, int da
     fail("et_generate_plan: %s at w=%d has no GPU kernel in this build", JE_method[method], w);
     return nullptr;
   }
-  if (data_strips < 1 || data_strips > lsec::kMaxK || parity_strips < 1 || parity_strips > kMaxM) {
-    fail("et_generate_plan: k=%d m=%d outside the engine's 1..%d x 1..%d", data_strips, parity_strips, lsec::kMaxK, kMaxM);
+  if (data_strips < 1 || parity_strips < 1 || data_strips + parity_strips > kMaxDevs) {
+    fail("et_generate_plan: k=%d m=%d: k+m outside the engine's 2..%d", data_strips, parity_strips, kMaxDevs);
     return nullptr;
   }
   if (packet_kind(kind) && best_size != file_size && file_size % data_strips == 0) {
@@ -3022,7 +3079,7 @@ int lsec_encode_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, 
   // (profiles/r01_v12_kbench_fused_magic.txt).
   const int kind = kernel_kind(plan->method, plan->w);
   const bool fuse = kind == KBYTEWISE || kind == KBITSLICED;
-  if (fuse && m <= 8 && !check_geometry(plan, block_size) && k + m <= lsec::kMaxMagicShards) {
+  if (fuse && m <= 8 && k <= lsec::kMaxK && !check_geometry(plan, block_size) && k + m <= lsec::kMaxMagicShards) {
     if (nstripes <= 0 || block_size == 0) return 0;
     const void *cells = nullptr;
     if (encode_cells(e, &cells)) return -1;

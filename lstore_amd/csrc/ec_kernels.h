@@ -21,8 +21,17 @@
 
 namespace lsec {
 
-constexpr int kMaxK = 64;   // data devices per stripe the kernels accept (LSEC_MAX_DEVS bounds k + m)
+constexpr int kMaxK = 64;   // input shards per launch (wider stripes: several launches, the later ones with
+                            // ApplyArgs::accumulate, over images in the grouped layout below)
 constexpr int kMaxR = 16;   // output shards per launch
+constexpr int kMaxW = 256;  // bitmatrix word size w (packets per super-packet) the kernels accept
+
+// Matrix images of stripes wider than kMaxK inputs are stored in groups of kMaxK input columns:
+// group g (inputs g*kMaxK ..) holds every row's cells / masks / products for its columns, rows in
+// order, so one launch per group reads a plain row-major image of its K_g columns.
+__host__ __device__ inline int image_groups(int K) { return (K + kMaxK - 1) / kMaxK; }
+// 32-bit words per bitmatrix mask: bit x of mask word q covers packet 32q + x of an input
+__host__ __device__ inline int mask_words(int w) { return (w + 31) / 32; }
 
 struct ShardRef {
   uint64_t base;    // device address of this shard in stripe 0
@@ -50,9 +59,11 @@ struct ApplyArgs {
   int nstripes;
   int packet;             // bitsliced / bitmatrix: packet size P (bytes)
   int64_t size;           // bytes per shard (chunk C)
-  const uint32_t *masks;  // bitmatrix: (R*w) x K words, bit x of [(r*w+l)*K + j] = B[r*w+l][j*w+x]
+  const uint32_t *masks;  // bitmatrix: (R*w) x K x mask_words(w) words, bit x of [((r*w+l)*K + j)*NW + q]
+                          //   = B[r*w+l][j*w + 32q + x]
                           // wordwise: R x K x w products, [(r*K + j)*w + b] = c_rj * x^b
   int w;                  // bitmatrix: packets per super-packet; wordwise: field width (16 / 32)
+  int accumulate;         // 1: out[r] ^= the result (the second and later input groups of a wide stripe)
   unsigned long long *magic_acc;  // encode only (bytewise, bitsliced): fused stripe magic over the K inputs then the
                                   // R outputs (2 x u64 per stripe, zeroed), see MagicArgs
   ShardRef in[kMaxK];
@@ -70,7 +81,9 @@ struct ApplyArgs {
 constexpr int kMaxMagicShards = kMaxK + kMaxR;
 
 struct MagicArgs {
-  int nshards;            // shards per stripe, in checksum order (LStore: data 0..k-1, parity 0..m-1)
+  int nshards;            // shards of this launch, in checksum order (LStore: data 0..k-1, parity 0..m-1)
+  int shard0;             // checksum index of sh[0] (wide stripes: one launch per kMaxMagicShards shards)
+  int total_shards;       // shards per stripe (0: nshards)
   int nstripes;
   int64_t size;           // bytes of each shard covered by this launch
   int64_t col0;           // column offset of those bytes inside the chunk (column-block staging)
@@ -138,7 +151,8 @@ hipError_t launch_bytewise(const ApplyArgs &a, hipStream_t stream, int grid_bloc
 hipError_t launch_bytewise_magic(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
 hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
 // generic GF(2) bitmatrix codes (liberation / blaum_roth / liber8tion, liberation.c; Cauchy at
-// w = 16 / 32): any w in LSEC_BITMATRIX_W, R <= 2 per launch
+// w = 16 / 32): w in LSEC_BITMATRIX_W by a kernel per w, any other 2 <= w <= kMaxW by the
+// LDS-staged kernel; R <= 2 per launch
 hipError_t launch_bitmatrix(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
 bool bitmatrix_w_supported(int w);
 // matrix codes over GF(2^16) / GF(2^32) (a.w), little-endian words, R <= 8: bit-sliced after

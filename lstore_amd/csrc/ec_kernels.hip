@@ -107,7 +107,7 @@ bool bitmatrix_w_supported(int w) {
 }
 
 hipError_t launch_bitmatrix(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
-  if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > 2 || !bitmatrix_w_supported(a.w) || !a.masks ||
+  if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > 2 || a.w < 2 || a.w > kMaxW || !a.masks ||
       a.packet <= 0 || a.packet % 4 != 0 || a.size % (static_cast<int64_t>(a.w) * a.packet) != 0)
     return hipErrorInvalidValue;
   if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(kBlock) void k_stripe_magic(MagicArgs a) {
   const int64_t C = a.size;
   const uint32_t tps = static_cast<uint32_t>((C + kTile - 1) / kTile);
   const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
-  const uint64_t L = static_cast<uint64_t>(a.nshards) * a.chunk;
+  const uint64_t L = static_cast<uint64_t>(a.total_shards ? a.total_shards : a.nshards) * a.chunk;
   for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
     const uint32_t s = t / tps;
     const int64_t off0 = static_cast<int64_t>(t - s * tps) * kTile + threadIdx.x * 16;
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(kBlock) void k_stripe_magic(MagicArgs a) {
           v.x = h.x;
           v.y = h.y;
         }
-        adler_add(v, L - static_cast<uint64_t>(i * a.chunk + a.col0 + o), as, bs);
+        adler_add(v, L - static_cast<uint64_t>(static_cast<int64_t>(a.shard0 + i) * a.chunk + a.col0 + o), as, bs);
       }
     }
     const uint32_t am = block_sum(static_cast<uint32_t>(as % kAdlerMod), red);

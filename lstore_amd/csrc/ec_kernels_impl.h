@@ -63,6 +63,19 @@ __device__ __forceinline__ LSEC_GLOBAL T *gptr_w(uint64_t addr) {
   return reinterpret_cast<LSEC_GLOBAL T *>(addr);
 }
 
+// Output stores.  ApplyArgs::accumulate (wave-uniform) XORs the result into what the output
+// holds: the second and later input groups of a stripe wider than kMaxK inputs.
+template <typename V>
+__device__ __forceinline__ void put_nt(int accumulate, uint64_t q, V v) {
+  if (accumulate) v ^= *gptr<V>(q);
+  __builtin_nontemporal_store(v, gptr_w<V>(q));
+}
+template <typename V>
+__device__ __forceinline__ void put(int accumulate, uint64_t q, V v) {
+  if (accumulate) v ^= *gptr<V>(q);
+  *gptr_w<V>(q) = v;
+}
+
 // ------------------------------------------------------------------ bytewise
 // 3-input XOR in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -368,7 +381,7 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
       for (int r = 0; r < R; ++r) {
         const uint64_t q = a.out[r].base + s * a.out[r].stride + off0;
 #pragma unroll
-        for (int it = 0; it < IT; ++it) __builtin_nontemporal_store(acc[it][r], gptr_w<V>(q + it * kStep));
+        for (int it = 0; it < IT; ++it) put_nt<V>(a.accumulate, q + it * kStep, acc[it][r]);
       }
     } else {
       // ragged last tile: C is a multiple of 8, so a 16-byte lane unit may be half full
@@ -400,12 +413,12 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
         for (int it = 0; it < IT; ++it) {
           const int64_t o = off0 + it * kStep;
           if (o + kLane <= C) {
-            *gptr_w<V>(q + o) = acc[it][r];
+            put<V>(a.accumulate, q + o, acc[it][r]);
           } else if (o < C) {
             u32x2 h;
             h.x = acc[it][r][0];
             h.y = acc[it][r][1];
-            *gptr_w<u32x2>(q + o) = h;
+            put<u32x2>(a.accumulate, q + o, h);
           }
         }
       }
@@ -505,7 +518,7 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
       for (int r = 0; r < R; ++r) {
         const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
 #pragma unroll
-        for (int x = 0; x < 8; ++x) __builtin_nontemporal_store(acc[r][x], gptr_w<V>(q + x * P));
+        for (int x = 0; x < 8; ++x) put_nt<V>(a.accumulate, q + x * P, acc[r][x]);
         if constexpr (MG) ml_add<8, DW>(ml, acc[r], static_cast<uint32_t>(K + r));
       }
     }
@@ -562,7 +575,80 @@ __global__ __launch_bounds__(kBlock) void k_bitmatrix(ApplyArgs a) {
     for (int r = 0; r < R; ++r) {
       const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
 #pragma unroll
-      for (int l = 0; l < W; ++l) __builtin_nontemporal_store(acc[r][l], gptr_w<uint32_t>(q + l * P));
+      for (int l = 0; l < W; ++l) put_nt<uint32_t>(a.accumulate, q + l * P, acc[r][l]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ bitmatrix, any w
+// Word sizes outside LSEC_BITMATRIX_W: a liberation plan with k > 31 gets the next prime w >= k
+// (37, 41, ..; erasure_tools.c:756-757), blaum_roth w = p - 1.  Per-w register tiles do not
+// scale there (acc[2][w] + e[w] registers), so a block stages its inputs in LDS instead.  A block
+// owns 1 KiB of packet-column space (4 B per lane); for each input it stages the words of up to
+// 64 packets of that column in LDS, and each of up to 64 output packets (registers) XORs the
+// staged words its mask selects: a loop over the mask's set bits (wave-uniform scalar mask
+// words), one LDS read per bit -- liberation rows have one or two bits per input block.  Output
+// packets beyond 64 take another pass over the inputs (w <= 64: one pass).
+template <int R>
+__global__ __launch_bounds__(kBlock) void k_bitmatrix_any(ApplyArgs a) {
+  constexpr int kChunk = 64;
+  __shared__ uint32_t stage[kChunk][kBlock];  // 64 KiB
+  const int K = a.K, W = a.w, NW = mask_words(a.w);
+  const uint32_t P = static_cast<uint32_t>(a.packet);
+  const uint32_t col_bytes = static_cast<uint32_t>(a.size / W);  // nsuper * P
+  constexpr uint32_t kTile = kBlock * 4;
+  const uint32_t tiles_per_stripe = (col_bytes + kTile - 1) / kTile;
+  const uint32_t ntiles = tiles_per_stripe * static_cast<uint32_t>(a.nstripes);
+  ConstU32 *masks = reinterpret_cast<ConstU32 *>(reinterpret_cast<uintptr_t>(a.masks));
+  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {  // block-uniform
+    const uint32_t s = t / tiles_per_stripe;
+    const uint32_t colb = (t - s * tiles_per_stripe) * kTile + threadIdx.x * 4;
+    const bool valid = colb < col_bytes;  // lanes past the end still join the barriers
+    const uint32_t sp = valid ? colb / P : 0;
+    const int64_t off = static_cast<int64_t>(sp) * W * P + (colb - sp * P);
+    for (int l0 = 0; l0 < W; l0 += kChunk) {
+      const int nl = min(kChunk, W - l0);
+      uint32_t acc[R][kChunk];
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int l = 0; l < kChunk; ++l) acc[r][l] = 0u;
+      for (int j = 0; j < K; ++j) {
+        const uint64_t p = a.in[j].base + s * a.in[j].stride + off;
+        for (int x0 = 0; x0 < W; x0 += kChunk) {
+          const int nx = min(kChunk, W - x0);
+          __syncthreads();  // the previous chunk's readers are done
+          for (int x = 0; x < nx; ++x)
+            stage[x][threadIdx.x] = valid ? __builtin_nontemporal_load(gptr<uint32_t>(p + static_cast<uint64_t>(x0 + x) * P)) : 0u;
+          __syncthreads();
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int l = 0; l < kChunk; ++l) {
+              if (l >= nl) continue;  // uniform; `continue` keeps the loop fully unrolled (acc in VGPRs)
+              const uint32_t mi = static_cast<uint32_t>(((r * W + l0 + l) * K + j) * NW + (x0 >> 5));
+              uint64_t m = masks[mi];
+              if (nx > 32) m |= static_cast<uint64_t>(masks[mi + 1]) << 32;
+              uint32_t v = 0;
+              while (m) {
+                v ^= stage[__builtin_ctzll(m)][threadIdx.x];
+                m &= m - 1;
+              }
+              acc[r][l] ^= v;
+            }
+        }
+      }
+      if (valid) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
+#pragma unroll
+          for (int l = 0; l < kChunk; ++l) {
+            if (l >= nl) continue;
+            put_nt<uint32_t>(a.accumulate, q + static_cast<uint64_t>(l0 + l) * P, acc[r][l]);
+          }
+        }
+      }
     }
   }
 }
@@ -646,12 +732,12 @@ __global__ __launch_bounds__(kBlock) void k_gfw_wordwise(ApplyArgs a) {
     for (int r = 0; r < R; ++r) {
       const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
       if (whole) {
-        __builtin_nontemporal_store(acc[r], gptr_w<V>(q));
+        put_nt<V>(a.accumulate, q, acc[r]);
       } else {
         u32x2 h;
         h.x = acc[r][0];
         h.y = acc[r][1];
-        *gptr_w<u32x2>(q) = h;
+        put<u32x2>(a.accumulate, q, h);
       }
     }
   }
@@ -732,7 +818,7 @@ __global__ __launch_bounds__(kBlock) void k_gfw_bitsliced(ApplyArgs a) {
     for (int r = 0; r < R; ++r) {
       const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
 #pragma unroll
-      for (int l = 0; l < W; ++l) __builtin_nontemporal_store(acc[r][l], gptr_w<uint32_t>(q + l * P));
+      for (int l = 0; l < W; ++l) put_nt<uint32_t>(a.accumulate, q + l * P, acc[r][l]);
     }
   }
 }
@@ -855,12 +941,12 @@ __device__ __forceinline__ void gfw_transposed_tiles(const ApplyArgs &a) {
         const int64_t o = base + static_cast<int64_t>(q) * kBlock * 16;
         const u32x4 v = {acc[r][4 * q], acc[r][4 * q + 1], acc[r][4 * q + 2], acc[r][4 * q + 3]};
         if (whole || o + 16 <= C) {
-          __builtin_nontemporal_store(v, gptr_w<u32x4>(q0 + o));
+          put_nt<u32x4>(a.accumulate, q0 + o, v);
         } else if (o + 8 <= C) {
           u32x2 h;
           h.x = v.x;
           h.y = v.y;
-          *gptr_w<u32x2>(q0 + o) = h;
+          put<u32x2>(a.accumulate, q0 + o, h);
         }
       }
     }
@@ -958,7 +1044,7 @@ hipError_t dispatch_bitmatrix(const ApplyArgs &a, hipStream_t st, int grid) {
   case WW: hipLaunchKernelGGL((k_bitmatrix<R, WW>), dim3(grid), dim3(kBlock), 0, st, a); break;
       LSEC_BITMATRIX_W(LSEC_BM_W)
 #undef LSEC_BM_W
-      default: return hipErrorInvalidValue;
+      default: hipLaunchKernelGGL((k_bitmatrix_any<R>), dim3(grid), dim3(kBlock), 0, st, a); break;
     }
     return hipGetLastError();
   } else {

@@ -334,7 +334,8 @@ bool make_bit_decode(int k, int m, int w, const std::vector<int> &bm, const std:
   }
   // output bit-rows: erased data i -> inv rows i*w..; erased coding c -> B_c x inv
   const int e = static_cast<int>(dp.erased.size());
-  masks.assign(static_cast<size_t>(e) * w * k, 0u);
+  const int nw = (w + 31) / 32;  // mask words per (bit-row, input), as lsec::mask_words
+  masks.assign(static_cast<size_t>(e) * w * k * nw, 0u);
   for (int r = 0; r < e; ++r) {
     const int id = dp.erased[r];
     for (int l = 0; l < w; ++l) {
@@ -348,7 +349,8 @@ bool make_bit_decode(int k, int m, int w, const std::vector<int> &bm, const std:
             for (int x = 0; x < words; ++x) row[x] ^= inv[c][x];
       }
       for (int c = 0; c < n; ++c)
-        if ((row[c / 64] >> (c % 64)) & 1) masks[static_cast<size_t>(r * w + l) * k + c / w] |= 1u << (c % w);
+        if ((row[c / 64] >> (c % 64)) & 1)
+          masks[(static_cast<size_t>(r * w + l) * k + c / w) * nw + (c % w) / 32] |= 1u << (c % w % 32);
     }
   }
   return true;

@@ -76,7 +76,7 @@ EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan",
            "lsec_set_kernel_variant", "lsec_set_host_devices", "lsec_hbm_copy_dev", "lsec_prepare_encode", "lsec_plan_jit")
 
 # read / inspect flags and stripe states (include/lstore_ec.h)
-READ_PARANOID, MAGIC_LEGACY, INSPECT_FIX, MAX_DEVS = 1, 2, 4, 64
+READ_PARANOID, MAGIC_LEGACY, INSPECT_FIX, MAX_DEVS = 1, 2, 4, 256
 STRIPE_OK, STRIPE_EMPTY, STRIPE_BAD_MAGIC, STRIPE_REPAIRED, STRIPE_LOST_MAGIC, STRIPE_LOST_MISMATCH = range(6)
 
 

@@ -43,7 +43,10 @@ def plan_entries():
     out += [(O.REED_SOL_R6_OP, 6, 2, 8), (O.REED_SOL_R6_OP, 10, 2, 8),
             (O.CAUCHY_GOOD, 2, 2, 8), (O.CAUCHY_GOOD, 32, 2, 8), (O.CAUCHY_GOOD, 3, 5, 8),
             (O.REED_SOL_VAN, 3, 5, 8), (O.REED_SOL_VAN, 32, 8, 8),
-            (O.LIBERATION, 6, 2, 7), (O.BLAUM_ROTH, 6, 2, 6), (O.LIBER8TION, 6, 2, 8)]
+            (O.LIBERATION, 6, 2, 7), (O.BLAUM_ROTH, 6, 2, 6), (O.LIBER8TION, 6, 2, 8),
+            # wide stripes (k + m = 128, 256 at w = 8) and word sizes past 32 (k > 31 liberation)
+            (O.REED_SOL_VAN, 100, 28, 8), (O.CAUCHY_GOOD, 100, 28, 8), (O.REED_SOL_VAN, 200, 56, 8),
+            (O.LIBERATION, 37, 2, 37), (O.BLAUM_ROTH, 36, 2, 36)]
     # wide fields (erasure_tools.c:806-811 accepts w = 16 / 32 for the matrix methods)
     for w in (16, 32):
         out += [(O.REED_SOL_VAN, 6, 3, w), (O.REED_SOL_VAN, 10, 4, w), (O.REED_SOL_R6_OP, 6, 2, w),
@@ -98,6 +101,12 @@ def cases():
     # bitmatrix families (not on the configs; fixtures for the next row)
     c += [(O.LIBERATION, 6, 2, 7, 7 * 64 * 4, 64, "splitmix"), (O.BLAUM_ROTH, 6, 2, 6, 6 * 64 * 4, 64, "splitmix"),
           (O.LIBER8TION, 6, 2, 8, 8 * 64 * 4, 64, "splitmix")]
+    # wide stripes: k + m = 128 and 256 at w = 8 (more inputs than one kernel launch takes), and
+    # liberation / blaum_roth past w = 32 (k > 31: w = 37, 67; blaum_roth w + 1 = 37 prime)
+    c += [(O.REED_SOL_VAN, 100, 28, 8, 4096, 0, "splitmix"), (O.CAUCHY_GOOD, 100, 28, 8, 4096, 64, "splitmix"),
+          (O.REED_SOL_VAN, 200, 56, 8, 2048, 0, "splitmix"), (O.CAUCHY_ORIG, 120, 8, 8, 2048, 32, "splitmix"),
+          (O.LIBERATION, 37, 2, 37, 37 * 32 * 2, 32, "splitmix"), (O.LIBERATION, 33, 2, 37, 37 * 64, 64, "affine"),
+          (O.LIBERATION, 67, 2, 67, 67 * 32, 32, "splitmix"), (O.BLAUM_ROTH, 36, 2, 36, 36 * 32 * 2, 32, "splitmix")]
     # wide fields: little-endian uint16 / uint32 elements (matrix codes), w*P super-packets (Cauchy)
     for w in (16, 32):
         for pat in ("affine", "splitmix"):

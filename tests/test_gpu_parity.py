@@ -54,9 +54,14 @@ def test_encode_block_matches_reference(cuda, golden):
 
 
 @pytest.mark.parametrize("method,k,w", [(L.LIBERATION, 7, 7), (L.LIBERATION, 11, 11), (L.BLAUM_ROTH, 10, 10),
-                                        (L.BLAUM_ROTH, 4, 4), (L.LIBER8TION, 8, 8), (L.LIBER8TION, 3, 8)])
+                                        (L.BLAUM_ROTH, 4, 4), (L.LIBER8TION, 8, 8), (L.LIBER8TION, 3, 8),
+                                        # w past the per-w kernels: the LDS-staged any-w kernel
+                                        (L.LIBERATION, 37, 37), (L.LIBERATION, 32, 37), (L.BLAUM_ROTH, 36, 36),
+                                        (L.BLAUM_ROTH, 40, 40),
+                                        # k > 64: input groups + accumulate; w > 64: two output passes
+                                        (L.LIBERATION, 67, 67), (L.LIBERATION, 71, 71)])
 def test_liberation_family_vs_reference(cuda, method, k, w):
-    """Generic GF(2) bitmatrix kernel vs the real reference (oracle/_ref) for every family member."""
+    """Generic GF(2) bitmatrix kernels vs the real reference (oracle/_ref) for every family member."""
     if not O.ref_available():
         pytest.skip("oracle/_ref not built")
     m, P = 2, 32
@@ -306,12 +311,19 @@ def test_xor_row_and_wide_shapes_vs_oracle(cuda, method, k, m, size):
 @pytest.mark.parametrize("method,k,m,size", [
     (L.REED_SOL_VAN, 40, 4, 8192),        # k beyond the compile-time K list: generic-K kernel
     (L.CAUCHY_GOOD, 40, 4, 8 * 64 * 4),
-    (L.REED_SOL_VAN, 48, 16, 4096),       # k + m = 64 (LSEC_MAX_DEVS), R = 16: two 8-row launches
-    (L.CAUCHY_ORIG, 30, 34, 8 * 32 * 2),  # k + m = 64 with more parity than data
+    (L.REED_SOL_VAN, 48, 16, 4096),       # R = 16: two 8-row launches
+    (L.CAUCHY_ORIG, 30, 34, 8 * 32 * 2),  # more parity than data
+    (L.REED_SOL_VAN, 70, 2, 4096),        # k > 64: two input groups, the second accumulating
+    (L.REED_SOL_VAN, 100, 28, 4104),      # k + m = 128, ragged 8-byte tail
+    (L.CAUCHY_GOOD, 100, 28, 8 * 64 * 2),
+    (L.CAUCHY_ORIG, 120, 8, 8 * 32 * 2),
+    (L.REED_SOL_VAN, 200, 56, 2048),      # k + m = 256: Jerasure's limit at w = 8 (reed_sol.c:247)
 ])
 def test_wide_stripes_vs_oracle(cuda, method, k, m, size):
-    """The widest stripes the engine takes (k + m <= 64): encode, stripe magic and erasures of
-    up to min(m, 6) devices, bit-exact vs the oracle and zlib."""
+    """Stripes up to k + m = 256 (LSEC_MAX_DEVS): encode from host and device memory, stripe
+    magic (in launches of 80 shards) and erasures spread over every input group, bit-exact vs
+    the oracle and zlib."""
+    import torch
     n = 2
     P = 64 if method == L.CAUCHY_GOOD else (32 if method == L.CAUCHY_ORIG else 0)
     st = np.zeros((n, k + m, size), dtype=np.uint8)
@@ -322,11 +334,21 @@ def test_wide_stripes_vs_oracle(cuda, method, k, m, size):
         for s in range(n):
             assert np.array_equal(st[s, k:], O.encode(method, st[s, :k], m, P)), s
             assert np.array_equal(magic[s], _je_magic(st[s])), s
+        data = torch.from_numpy(st[:, :k].copy()).cuda()
+        par = torch.zeros((n, m, size), dtype=torch.uint8, device="cuda")
+        p.encode_dev(data, par)
+        assert np.array_equal(par.cpu().numpy(), st[:, k:])
         full = st.copy()
-        for pat in ([0], [k + m - 1], list(range(min(m, 6))), [1, k, k + 1][: m]):
+        spread = list(range(0, k + m, max(1, (k + m) // m)))[:m]  # one erasure per stretch of devices
+        for pat in ([0], [k + m - 1], list(range(min(m, 6))), [1, k, k + 1][: m], spread):
             st[:, pat] = 0x42
             p.decode_stripes(st, pat)
             assert np.array_equal(st, full), pat
+        pat = spread
+        dev = torch.from_numpy(full.copy()).cuda()
+        dev[:, pat] = 0x42
+        p.decode_dev(dev[:, :k], dev[:, k:], pat)
+        assert np.array_equal(dev.cpu().numpy(), full)
 
 
 @pytest.mark.parametrize("k,m,size", [
@@ -366,12 +388,11 @@ def test_xor_network_vs_oracle(cuda, k, m, size):
 
 
 def test_stripe_width_limits_are_errors(cuda):
-    """m > 64 (LSEC_MAX_DEVS) is refused with a message, never written past a table."""
-    k, m, size = 4, 65, 4096
-    with L.Plan.new(L.REED_SOL_VAN, size, k, m, 8, 8, 8) as p:
-        assert p.form_encoding_matrix() == 0
+    """k + m > 256 (LSEC_MAX_DEVS) is refused with a message, never written past a table."""
+    k, m, size = 200, 57, 4096
+    with L.Plan.new(L.REED_SOL_VAN, size, k, m, 16, 8, 8) as p:
         st = np.zeros((1, k + m, size), np.uint8)
-        with pytest.raises(L.ErasureError, match="m=65"):
+        with pytest.raises(L.ErasureError, match="k\\+m"):
             p.encode_stripes(st)
 
 

@@ -49,6 +49,8 @@ def test_reference_plumbing_layout(built):
     (L.CAUCHY_GOOD, 6, 3, 16384, 1, 0),       # cjerase_16k.ex3 (sample_exnodes)
     (L.CAUCHY_GOOD, 10, 4, 262144, 3, 2),
     (L.REED_SOL_VAN, 20, 6, 1 << 20, 1, 0),   # column-block staging
+    (L.REED_SOL_VAN, 100, 28, 4096, 1, 0),    # k + m = 128: input groups, magic in 80-shard launches
+    (L.CAUCHY_GOOD, 70, 2, 8192, 2, 1),
 ])
 def test_segment_write_matches_reference(cuda, method, k, m, chunk, n_shift, first):
     n_str = 12 if chunk <= 262144 else 3
@@ -100,4 +102,23 @@ def test_segment_read_quorum_repair_and_brute_force(cuda):
         assert status[1] == 1 and np.array_equal(out[1], data[1])
         # an unreadable device: every stripe rebuilds through decode
         out, status, bad = p.segment_read(img, N, C, shift, 0, missing=(3,))
+        assert bad == 0 and np.array_equal(out, data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,k,m,C", [(L.REED_SOL_VAN, 100, 28, 4096), (L.CAUCHY_GOOD, 70, 2, 8192)])
+def test_wide_segment_read_repairs(cuda, method, k, m, C):
+    """Wide segments (k + m = 128 / 72): a stale magic on up to m devices of a stripe is voted
+    out, the stripe rebuilt from the others and checked against its magic."""
+    N, shift = 6, 1
+    n = k + m
+    data = np.stack([stripe(k, C, s + 40) for s in range(N)])
+    lc = C + 4
+    with L.Plan.for_chunk(method, k, m, C) as p:
+        img = p.segment_write(data, shift, 0)
+        rng = np.random.default_rng(k)
+        for s in range(N):
+            for d in rng.permutation(n)[: min(m, 1 + s % 3)]:
+                img[d, s * lc] ^= 0x11
+        out, status, bad = p.segment_read(img, N, C, shift, 0)
         assert bad == 0 and np.array_equal(out, data)
