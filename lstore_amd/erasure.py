@@ -62,6 +62,11 @@ PlanStruct._fields_ = [
 ]
 
 
+class IoVec(C.Structure):
+    """struct iovec (sys/uio.h), as lsec_segment_write_iov takes the tbuf's pieces."""
+    _fields_ = [("iov_base", C.c_void_p), ("iov_len", C.c_size_t)]
+
+
 class ShardRef(C.Structure):
     """lsec_shard_t: shard i of stripe s lives at base + s*stride (device memory)."""
     _fields_ = [("base", C.c_void_p), ("stride", C.c_longlong)]
@@ -71,7 +76,7 @@ class ShardRef(C.Structure):
 EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan", "et_destroy_plan",
            "et_encode", "et_decode", "et_encode_stripes", "et_decode_stripes", "lsec_encode_dev",
            "lsec_decode_dev", "et_encode_stripes_magic", "et_stripes_magic", "lsec_encode_magic_dev",
-           "lsec_stripe_magic_dev", "lsec_segment_write", "lsec_segment_read", "lsec_segment_inspect",
+           "lsec_stripe_magic_dev", "lsec_segment_write", "lsec_segment_write_iov", "lsec_segment_read", "lsec_segment_inspect",
            "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count", "lsec_last_error", "lsec_plan_kernel",
            "lsec_set_kernel_variant", "lsec_set_host_devices", "lsec_hbm_copy_dev", "lsec_prepare_encode", "lsec_plan_jit")
 
@@ -134,6 +139,7 @@ def lib():
     L.lsec_encode_magic_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.c_void_p, C.c_void_p]
     L.lsec_stripe_magic_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.c_void_p, C.c_void_p]
     L.lsec_segment_write.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_void_p]
+    L.lsec_segment_write_iov.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_void_p]
     L.lsec_segment_read.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_int, C.c_void_p,
                                     C.c_void_p]
     L.lsec_segment_inspect.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -347,6 +353,26 @@ class Plan:
         ptrs = self._ptr_array([dev[i].ctypes.data for i in range(n)])
         _check(lib().lsec_segment_write(self._p, data.ctypes.data, n_str, size, n_shift, first_stripe, ptrs),
                "lsec_segment_write")
+        return dev
+
+    def segment_write_iov(self, pieces, nstripes: int, chunk: int, n_shift: int = 1,
+                          first_stripe: int = 0) -> np.ndarray:
+        """pieces: the user data as a scatter list of uint8 arrays, or ints for error pages of that
+        many bytes -> device images uint8 [k+m, N*(C+4)] (lsec_segment_write_iov)."""
+        n = self.k + self.m
+        iov = (IoVec * max(1, len(pieces)))()
+        keep = []
+        for i, pc in enumerate(pieces):
+            if isinstance(pc, (int, np.integer)):
+                iov[i].iov_base, iov[i].iov_len = None, int(pc)
+            else:
+                pc = np.ascontiguousarray(pc, dtype=np.uint8)
+                keep.append(pc)
+                iov[i].iov_base, iov[i].iov_len = pc.ctypes.data, pc.nbytes
+        dev = np.zeros((n, nstripes * (chunk + 4)), dtype=np.uint8)
+        ptrs = self._ptr_array([dev[i].ctypes.data for i in range(n)])
+        _check(lib().lsec_segment_write_iov(self._p, iov, len(pieces), nstripes, chunk, n_shift, first_stripe, ptrs),
+               "lsec_segment_write_iov")
         return dev
 
     def segment_read(self, dev: np.ndarray, nstripes: int, chunk: int, n_shift: int = 1, first_stripe: int = 0,

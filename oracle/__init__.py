@@ -83,6 +83,9 @@ def ref():
         lib.ref_segment_write.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong,
                                           C.c_void_p]
         lib.ref_segment_write.restype = None
+        lib.ref_segment_write_iov.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                              C.c_longlong, C.c_void_p]
+        lib.ref_segment_write_iov.restype = None
         lib.ref_segment_inspect.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         lib.ref_segment_inspect.restype = None
@@ -225,6 +228,22 @@ class RefPlan:
         ptrs = _ptrs([dev[i] for i in range(n)])
         data = np.ascontiguousarray(data)
         self.lib.ref_segment_write(self.h, data.ctypes.data, nstripes, chunk, n_shift, first_stripe, ptrs)
+        return dev
+
+    def segment_write_iov(self, pieces, nstripes, chunk, n_shift=1, first_stripe=0):
+        """segjerase_write_func's scatter-list / straddle / error-page handling restated over the
+        real jerasure.  pieces: uint8 arrays, or ints for error pages of that many bytes."""
+        n = self.k + self.m
+        dev = np.zeros((n, nstripes * (chunk + 4)), dtype=np.uint8)
+        keep = [np.ascontiguousarray(pc, dtype=np.uint8) for pc in pieces if not isinstance(pc, (int, np.integer))]
+        bases, it = [], iter(keep)
+        for pc in pieces:
+            bases.append(0 if isinstance(pc, (int, np.integer)) else next(it).ctypes.data)
+        lens = np.array([int(pc) if isinstance(pc, (int, np.integer)) else np.asarray(pc).size for pc in pieces],
+                        dtype=np.int64)
+        base_arr = (C.c_void_p * max(1, len(pieces)))(*bases)
+        self.lib.ref_segment_write_iov(self.h, base_arr, lens.ctypes.data, len(pieces), nstripes, chunk, n_shift,
+                                       first_stripe, _ptrs([dev[i] for i in range(n)]))
         return dev
 
     def segment_inspect(self, buf, nstripes, chunk, magic_cksum=1, do_fix=0, brute=None):

@@ -261,6 +261,75 @@ void ref_segment_write(ref_plan_t *p, const char *data, int nstripes, int chunk,
     free(ptr);
 }
 
+/* segjerase_write_func's user-buffer handling (segment/jerasure.c:1786-1825) restated: the
+ * data arrives as a scatter list of n_iov pieces (the cache pages of the tbuf; base NULL = an
+ * error page).  For each stripe of k*C bytes, as tbx_tbuf_next sees it:
+ *   - inside one piece (tbv.n_iov == 1): the data chunk pointers point into it (:1818-1819);
+ *   - straddling pieces: the bytes are first copied into a contiguous buffer (:1795-1811) and
+ *     the chunk pointers point into that copy (:1820-1821);
+ *   - a stripe whose first piece is an error page: every data chunk pointer is a zero chunk
+ *     (:1816, :1823-1831) -- zeros are encoded and written.
+ * Error pages inside a straddling stripe (after its first piece) read as zeros here: the
+ * reference's tbx_tbuf_copy would read through the NULL base. */
+void ref_segment_write_iov(ref_plan_t *p, char **iov_base, const long long *iov_len, int n_iov, int nstripes,
+                           int chunk, int n_shift, long long first_stripe, char **dev)
+{
+    int k = p->k, m = p->m, n = k + m;
+    size_t C = (size_t)chunk, lchunk = C + 4, dsize = (size_t)k * C;
+    char **ptr = (char **)malloc(sizeof(char *) * n);
+    char *parity = (char *)malloc(C * m);
+    char *straddle = (char *)malloc(dsize);
+    char *empty = (char *)calloc(1, C);
+    int pi = 0;              /* piece holding byte `off` */
+    long long pstart = 0;    /* offset of piece pi */
+    for (int s = 0; s < nstripes; s++) {
+        long long off = (long long)s * (long long)dsize;
+        while (pi < n_iov && pstart + iov_len[pi] <= off) pstart += iov_len[pi++];
+        if (pi >= n_iov) break;  /* scatter list shorter than the stripes: nothing more to write */
+        char *base;
+        if (iov_base[pi] == NULL) {
+            for (int j = 0; j < k; j++) ptr[j] = empty;
+        } else {
+            if (pstart + iov_len[pi] >= off + (long long)dsize) {
+                base = iov_base[pi] + (off - pstart);
+            } else {
+                size_t got = 0;
+                int q = pi;
+                long long qs = pstart;
+                while (got < dsize && q < n_iov) {
+                    long long from = off + (long long)got - qs;
+                    size_t take = (size_t)(iov_len[q] - from);
+                    if (take > dsize - got) take = dsize - got;
+                    if (iov_base[q]) memcpy(straddle + got, iov_base[q] + from, take);
+                    else memset(straddle + got, 0, take);
+                    got += take;
+                    qs += iov_len[q++];
+                }
+                if (got < dsize) memset(straddle + got, 0, dsize - got);
+                base = straddle;
+            }
+            for (int j = 0; j < k; j++) ptr[j] = base + (size_t)j * C;
+        }
+        for (int r = 0; r < m; r++) ptr[k + r] = parity + (size_t)r * C;
+        ref_plan_encode(p, ptr, chunk);
+        unsigned long ck = adler32(0L, Z_NULL, 0);
+        for (int i = 0; i < n; i++) ck = adler32(ck, (unsigned char *)ptr[i], chunk);
+        unsigned char magic[4];
+        for (int i = 0; i < 4; i++) { magic[i] = ck & 255; ck >>= 8; }
+        long long ss = first_stripe + s;
+        for (int i = 0; i < n; i++) {
+            int j = (int)((i + ss * n_shift) % n);
+            char *slot = dev[i] + (size_t)s * lchunk;
+            memcpy(slot, magic, 4);
+            memcpy(slot + 4, ptr[j], C);
+        }
+    }
+    free(empty);
+    free(straddle);
+    free(parity);
+    free(ptr);
+}
+
 /* ---------------------------------------------------------------- verification / repair
  * The segment's verification helpers, restated over the real jerasure decode (ref_plan_decode)
  * and zlib, since segment/jerasure.c cannot be built here:

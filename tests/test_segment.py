@@ -122,3 +122,79 @@ def test_wide_segment_read_repairs(cuda, method, k, m, C):
                 img[d, s * lc] ^= 0x11
         out, status, bad = p.segment_read(img, N, C, shift, 0)
         assert bad == 0 and np.array_equal(out, data)
+
+
+# ---------------------------------------------------------------- scatter lists (tbuf pieces)
+def scatter(data, cuts, error_pieces):
+    """Split the flat user bytes at `cuts`; pieces whose index is in `error_pieces` become error
+    pages (ints: their length)."""
+    flat = data.reshape(-1)
+    bounds = [0] + sorted(cuts) + [flat.size]
+    pieces = []
+    for i in range(len(bounds) - 1):
+        pc = flat[bounds[i]:bounds[i + 1]]
+        pieces.append(int(pc.size) if i in error_pieces else pc.copy())
+    return pieces
+
+
+def flatten_like_reference(pieces, n_str, k, chunk):
+    """What segjerase_write_func encodes for each stripe of a scatter list (segment/jerasure.c:
+    1786-1831): the stripe's bytes, except a stripe whose first piece is an error page is all
+    zeros; error pages inside a straddling stripe read as zeros."""
+    flat = np.concatenate([np.zeros(pc, np.uint8) if isinstance(pc, int) else pc for pc in pieces])
+    starts = np.cumsum([0] + [pc if isinstance(pc, int) else pc.size for pc in pieces])
+    out = flat[: n_str * k * chunk].reshape(n_str, k, chunk).copy()
+    for s in range(n_str):
+        p = int(np.searchsorted(starts, s * k * chunk, side="right")) - 1
+        if isinstance(pieces[p], int):
+            out[s] = 0
+    return out
+
+
+SCATTER_CASES = [
+    # (cuts as fractions of a stripe, error pieces)
+    ([], set()),                          # one piece: in place
+    ([0.5, 1.0, 2.25, 2.75], set()),      # straddles at half / quarter stripes
+    ([1.0, 2.0, 3.5], {1}),               # stripe 1 starts in an error page -> zeros
+    ([0.3, 0.6, 4.0], {1}),               # error page inside a straddling stripe
+    ([2.0, 2.002], {1}),                  # a small error page at a stripe start
+]
+
+
+def _cut_points(k, chunk, fracs):
+    dsize = k * chunk
+    return [int(round(f * dsize)) // 8 * 8 for f in fracs]
+
+
+def test_scatter_write_restatement(built):
+    """The harness's scatter-list write (ref_segment_write_iov) equals the contiguous reference
+    write of the bytes segjerase_write_func encodes (CPU only)."""
+    if not O.ref_available():
+        pytest.skip("oracle/_ref not built")
+    k, m, C, N = 6, 3, 1024, 6
+    data = np.stack([stripe(k, C, s + 3) for s in range(N)])
+    rp = O.RefPlan(O.REED_SOL_VAN, k, m)
+    for fracs, errs in SCATTER_CASES:
+        pieces = scatter(data, _cut_points(k, C, fracs), errs)
+        got = rp.segment_write_iov(pieces, N, C, 1, 2)
+        want = rp.segment_write(flatten_like_reference(pieces, N, k, C), N, C, 1, 2)
+        assert np.array_equal(got, want), (fracs, errs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,k,m,chunk", [(L.REED_SOL_VAN, 6, 3, 4096), (L.CAUCHY_GOOD, 6, 3, 16384),
+                                              (L.REED_SOL_VAN, 10, 4, 65536)])
+def test_segment_write_iov_matches_reference(cuda, method, k, m, chunk):
+    """lsec_segment_write_iov vs the restated segjerase_write_func over the real jerasure on
+    scatter lists with straddling stripes and error pages: identical device images."""
+    N = 6
+    data = np.stack([stripe(k, chunk, s + 11) for s in range(N)])
+    with L.Plan.for_chunk(method, k, m, chunk) as p:
+        rp = O.RefPlan(method, k, m, 8, p.packet_size)
+        for fracs, errs in SCATTER_CASES:
+            pieces = scatter(data, _cut_points(k, chunk, fracs), errs)
+            ours = p.segment_write_iov(pieces, N, chunk, 2, 5)
+            ref = rp.segment_write_iov(pieces, N, chunk, 2, 5)
+            assert np.array_equal(ours, ref), (fracs, errs)
+        with pytest.raises(L.ErasureError, match="bytes in the scatter list"):
+            p.segment_write_iov([data.reshape(-1)[:-8]], N, chunk)
