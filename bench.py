@@ -359,6 +359,20 @@ class HipEngine:
                 "decode_vs_probe": round((dec_hbm / t_dec) / (2 * nb / t_probe), 3)}
             del src, dst
             self.drop()
+            # the decode's own traffic mix without its arithmetic: a raid4 (k+1) decode of shard 0
+            # is a plain XOR of the k survivors -- k reads : 1 write per column, as the decode
+            xplan = self.L.Plan.for_chunk(E.JE_METHOD_NAMES.index("raid4"), k, 1, C)
+            xd = torch.empty((N, k, C), dtype=torch.uint8, device=self.dev)
+            xp = torch.empty((N, 1, C), dtype=torch.uint8, device=self.dev)
+            refs, n, size = xplan.tensor_refs(xd, xp)
+            t_xor = timed(lambda: xplan.decode_dev_refs(refs, n, size, [0], self.sh))
+            out["hbm_copy_ref"]["xor_read_mix"] = {
+                "what": "raid4(k+1) decode of shard 0 over N stripes: the decode's k:1 read:write bytes, XOR only",
+                "frac": round(dec_hbm / t_xor / HBM_PEAK, 4),
+                "decode_vs_xor": round(t_xor / t_dec, 3)}
+            xplan.close()
+            del xd, xp
+            self.drop()
         if rank == 0 and world == 1:
             # the reference CPU path is timed at N=1 only (at N>1 it would only delay the ranks' exit)
             out["cpu_baseline"] = None if a.no_cpu else cpu_baseline(self.method, k, m, C, self.P, a.lost, a.cpu_seconds)
