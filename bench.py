@@ -34,6 +34,7 @@ Also reported (same JSON line):
 Every run checks parity bit-exactly against the reference (oracle/_ref) on sampled stripes.
 """
 import argparse
+import glob
 import json
 import os
 import socket
@@ -71,6 +72,8 @@ def parse(argv=None):
     ap.add_argument("--no-layout-ab", action="store_true", help="skip the padded-layout comparison")
     ap.add_argument("--no-copy-ref", action="store_true", help="skip the device-copy HBM reference")
     ap.add_argument("--json-out", default="", help="also write rank 0's JSON line to this file")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the in-run rocprofv3 PMC traffic passes (roofline.traffic from a committed profile)")
     return ap.parse_args(argv)
 
 
@@ -160,6 +163,70 @@ def pmc_traffic(k, m, C, N, kernel_kind, pad):
             if name.startswith(prefix):
                 return int(v["traffic_per_stripe"] * N), os.path.relpath(f, ROOT)
     return None, None
+
+
+def _run_killable(cmd, timeout, **kw):
+    """subprocess.run in its own process group, the whole group killed on timeout (rocprofv3
+    runs the profiled program as its own child)."""
+    import signal
+    import subprocess
+
+    p = subprocess.Popen(cmd, start_new_session=True, **kw)
+    try:
+        return p.wait(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.wait()
+        return None
+
+
+def pmc_traffic_live(a, N):
+    """roofline.traffic measured for this run's configuration: two rocprofv3 --pmc passes
+    (FETCH_SIZE, then WRITE_SIZE: they do not fit one pass, MI355X_MICROARCH.md) over a 1-step
+    child run of the same geometry, started before this process touches the GPU.  FETCH_SIZE and
+    WRITE_SIZE are in KiB; gfx950 counts a coalesced streaming read at half its bytes, so FETCH is
+    doubled (the guide's HBM section; checked against the algorithmic bytes in
+    profiles/*_pmc_traffic.json).  The encode kernel is the engine kernel that writes the most.
+    None when rocprofv3 is missing, this process already runs under a profiler, or a pass fails."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+
+    if shutil.which("rocprofv3") is None or os.environ.get("LSEC_BENCH_PMC_CHILD"):
+        return None
+    if any(k.startswith("ROCPROF") for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return None
+    args = ["--method", a.method, "--k", str(a.k), "--m", str(a.m), "--chunk", str(a.chunk), "--stripes", str(N),
+            "--pad", str(a.pad), "--variant", a.variant, "--lost", str(a.lost), "--steps", "1", "--warmup", "0",
+            "--no-cpu", "--no-host-path", "--no-layout-ab", "--no-copy-ref", "--no-pmc"]
+    vals = {}
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(td, counter)
+            cmd = ["rocprofv3", "--pmc", counter, "--kernel-trace", "--output-format", "csv", "-d", out, "-o", "pmc",
+                   "--", sys.executable, os.path.abspath(__file__)] + args
+            rc = _run_killable(cmd, 240, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp", LSEC_BENCH_PMC_CHILD="1"),
+                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            if rc != 0:
+                return None
+            for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        name = row["Kernel_Name"]
+                        if row.get("Counter_Name") == counter and "lsec" in name and "hbm_copy" not in name:
+                            vals.setdefault((name, counter), []).append(float(row["Counter_Value"]) * 1024)
+    med = {key: sorted(v)[len(v) // 2] for key, v in vals.items()}
+    writes = {name: v for (name, c), v in med.items() if c == "WRITE_SIZE"}
+    if not writes:
+        return None
+    name = max(writes, key=writes.get)
+    fetch = med.get((name, "FETCH_SIZE"))
+    if fetch is None:
+        return None
+    traffic = 2 * fetch + writes[name]
+    return {"kernel": name, "fetch_raw": fetch, "write": writes[name], "traffic_per_stripe": traffic / N,
+            "launches": len(vals.get((name, "FETCH_SIZE"), []))}
 
 
 def host_path_rate(plan, k, m, C, lost, nstripes, pinned=False, reps=3):
@@ -387,6 +454,11 @@ class HipEngine:
         return "gf8_bytewise (encode)" if self.kernel == 1 else "gf8_bitsliced (encode)"
 
     def traffic(self, N):
+        live = getattr(self.a, "traffic_live", None)
+        if live:
+            return int(live["traffic_per_stripe"] * N), (
+                "measured in this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over a 1-step child "
+                f"run of this configuration, FETCH x2 (gfx950), kernel {live['kernel']}, median of {live['launches']} launches")
         return pmc_traffic(self.a.k, self.a.m, self.a.chunk, N, self.kernel, self.a.pad)
 
     def close(self):
@@ -565,7 +637,12 @@ def launch(a, engine_cls=HipEngine):
 
 
 def main():
-    sys.exit(launch(parse()))
+    a = parse()
+    if a.gpus == 1 and os.environ.get("WORLD_SIZE", "1") == "1" and not a.no_pmc:
+        # before this process touches the GPU: the counter passes run the same configuration as
+        # child processes under rocprofv3
+        a.traffic_live = pmc_traffic_live(a, a.total_stripes or a.stripes)
+    sys.exit(launch(a))
 
 
 if __name__ == "__main__":
