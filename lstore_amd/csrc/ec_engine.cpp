@@ -13,6 +13,7 @@
 // HIP kernels in ec_kernels.hip.  If the GPU is unavailable the calls fail (status -1, or
 // abort() from the void encode_block fn-pointer).
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <strings.h>
 
 #include <algorithm>
@@ -1834,27 +1835,178 @@ bool regular_refs(const std::vector<uint64_t> &a, int nstripes, size_t per, std:
   return true;
 }
 
-// Waits until flag reaches v (wrapping u32 sequence): spin first (the usual call completes in
-// ~10-20 us), then yield, then sleep, so many waiting callers do not starve the one whose work
-// is done of a CPU.  Bounded: after `limit` the caller checks its stream for an error.
+// ---------------------------------------------------------------- waiting for completion flags
+// CPUs this process may keep busy: the affinity mask, capped by the cgroup CPU quota (a GPU box
+// may show the whole machine's CPUs and grant a share of them).
+int usable_cpus() {
+  static const int n = [] {
+    int c = 1;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) c = std::max(1, CPU_COUNT(&set));
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      long long period = 0;
+      if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0)
+        c = std::min<long long>(c, std::max(1LL, (atoll(q) + period - 1) / period));
+      fclose(f);
+    }
+    return c;
+  }();
+  return n;
+}
+
+// Completion waits.  LStore calls encode_block from up to 300 pool threads; a waiter that spins
+// (or yields) holds a CPU, and with more waiters than CPUs the spinning starves the threads whose
+// calls are done -- on a cgroup quota it also burns the quota and gets the whole process
+// throttled.  So at most half the usable CPUs spin; every other waiter parks on its own
+// condition variable, and one poller thread watches the parked waiters' flags and wakes them.
+class FlagWaits {
+ public:
+  static FlagWaits &get() {
+    static FlagWaits *w = new FlagWaits();  // leaked: the poller thread outlives static destruction
+    return *w;
+  }
+
+  // Waits until *flag reaches want (wrapping u32 sequence: want - *flag <= 0), or up to `slice`;
+  // true when reached.  Callers loop, doing their own checks between slices.
+  bool wait(const unsigned *flag, unsigned want, std::chrono::microseconds slice) {
+    if (reached(flag, want)) return true;
+    if (spin_only_) {  // LSEC_WAIT=spin (A/B runs): every waiter spins, then yields, then naps
+      const auto t0 = std::chrono::steady_clock::now();
+      for (unsigned i = 0;; ++i) {
+        if (reached(flag, want)) return true;
+        if (i < 500) {
+          __builtin_ia32_pause();
+          continue;
+        }
+        const auto dt = std::chrono::steady_clock::now() - t0;
+        if (dt > slice) return false;
+        if (dt < std::chrono::microseconds(200)) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
+      }
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    // spin only while waits are short: under load (waits of 100s of us) a spinner holds a CPU
+    // for nothing that the callers' copies need
+    const bool short_waits = !adapt_ || recent_us_.load(std::memory_order_relaxed) < 2 * spin_.count();
+    const int active = spinners_.fetch_add(1, std::memory_order_relaxed) + 1;
+    if (short_waits && active <= spin_limit_) {
+      for (unsigned i = 1;; ++i) {
+        if (reached(flag, want)) {
+          spinners_.fetch_sub(1, std::memory_order_relaxed);
+          note(t0);
+          return true;
+        }
+        __builtin_ia32_pause();
+        if ((i & 63) == 0 && std::chrono::steady_clock::now() - t0 > spin_) break;
+      }
+    }
+    spinners_.fetch_sub(1, std::memory_order_relaxed);
+    Parked pk{flag, want};
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      parked_.push_back(&pk);
+    }
+    cv_.notify_one();
+    {
+      std::unique_lock<std::mutex> lk(pk.m);
+      pk.cv.wait_for(lk, slice, [&] { return pk.woken; });
+    }
+    {
+      // still listed: take it out (the poller wakes only listed waiters, under mu_)
+      std::lock_guard<std::mutex> lk(mu_);
+      auto it = std::find(parked_.begin(), parked_.end(), &pk);
+      if (it != parked_.end()) parked_.erase(it);
+    }
+    if (!reached(flag, want)) return false;
+    note(t0);
+    return true;
+  }
+
+ private:
+  struct Parked {
+    const unsigned *flag;
+    unsigned want;
+    std::mutex m;
+    std::condition_variable cv;
+    bool woken = false;
+  };
+
+  // moving average of completed waits (us), 1/8 weight per sample
+  void note(std::chrono::steady_clock::time_point t0) {
+    const long us = static_cast<long>(
+        std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count());
+    const long old = recent_us_.load(std::memory_order_relaxed);
+    recent_us_.store(old + (us - old) / 8, std::memory_order_relaxed);
+  }
+
+  static bool reached(const unsigned *flag, unsigned want) {
+    return static_cast<int>(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - want) >= 0;
+  }
+
+  FlagWaits() {
+    const char *n = getenv("LSEC_WAIT_SPINNERS"), *us = getenv("LSEC_WAIT_SPIN_US");
+    // defaults from tools/gpu_wait_sweep.sh (profiles/r02_v22_wait_sweep.jsonl): a quarter of the
+    // usable CPUs spin, for up to 30 us (an unloaded call completes in 14-20 us)
+    spin_limit_ = n ? std::max(0, atoi(n)) : std::max(1, usable_cpus() / 4);
+    spin_ = std::chrono::microseconds(us ? std::max(0, atoi(us)) : 30);
+    const char *w = getenv("LSEC_WAIT"), *ad = getenv("LSEC_WAIT_ADAPT");
+    spin_only_ = w && strcmp(w, "spin") == 0;
+    adapt_ = !ad || atoi(ad) != 0;
+    if (!spin_only_) std::thread([this] { poll(); }).detach();
+  }
+
+  void poll() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return !parked_.empty(); });
+      for (size_t i = 0; i < parked_.size();) {
+        Parked *p = parked_[i];
+        if (reached(p->flag, p->want)) {
+          {
+            std::lock_guard<std::mutex> g(p->m);
+            p->woken = true;
+          }
+          p->cv.notify_one();  // under mu_: the waiter cannot unlist and free it meanwhile
+          parked_[i] = parked_.back();
+          parked_.pop_back();
+        } else {
+          ++i;
+        }
+      }
+      if (!parked_.empty()) {  // flags are written by the GPU: poll, a few us apart
+        lk.unlock();
+        for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+        std::this_thread::yield();
+        lk.lock();
+      }
+    }
+  }
+
+  int spin_limit_ = 1;                   // waiters allowed to spin at once (LSEC_WAIT_SPINNERS)
+  std::chrono::microseconds spin_{100};  // how long one spins before parking (LSEC_WAIT_SPIN_US)
+  bool spin_only_ = false;
+  bool adapt_ = true;  // no spinning while recent waits are long (LSEC_WAIT_ADAPT=0: always)
+  std::atomic<int> spinners_{0};
+  std::atomic<long> recent_us_{0};
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Parked *> parked_;
+};
+
+// Waits until flag reaches v (wrapping u32 sequence) through FlagWaits.  Bounded: after 2 s
+// the caller checks its stream for an error.
 bool wait_flag(const unsigned *flag, unsigned v, hipStream_t st, int *rc) {
   const auto t0 = std::chrono::steady_clock::now();
-  for (unsigned spins = 0;; ++spins) {
-    if (static_cast<int>(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - v) >= 0) return true;
-    if (spins < 500) {
-      __builtin_ia32_pause();
-      continue;
-    }
-    const auto dt = std::chrono::steady_clock::now() - t0;
-    if (dt > std::chrono::seconds(2)) {
+  while (!FlagWaits::get().wait(flag, v, std::chrono::milliseconds(1))) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
       const hipError_t e = hipStreamSynchronize(st);
       if (static_cast<int>(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - v) >= 0) return true;
       *rc = fail("zero-copy call: completion flag never came (%s)", hipGetErrorString(e));
       return false;
     }
-    if (dt < std::chrono::microseconds(200)) std::this_thread::yield();
-    else std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
+  return true;
 }
 
 // ---------------------------------------------------------------- stripe server (host side)
@@ -1894,7 +2046,11 @@ class StripeServer {
     const long long unit = kind == KBITSLICED ? 8LL * p->packet_size : 16;
     const long long max_len = direct ? C : static_cast<long long>(kSlotBytes / nio) / unit * unit;
     if (max_len < std::min<long long>(unit, C)) return 1;
-    long long len = std::min(std::max<long long>(unit, 4096 / unit * unit), max_len);
+    static const long long target = [] {  // column bytes per part (LSEC_SRV_PART_KB, A/B runs)
+      const char *v = getenv("LSEC_SRV_PART_KB");
+      return v ? std::max(1LL, atoll(v)) << 10 : 4096LL;
+    }();
+    long long len = std::min(std::max<long long>(unit, target / unit * unit), max_len);
     if ((C + len - 1) / len > kMaxParts) {
       len = ((C + kMaxParts - 1) / kMaxParts + unit - 1) / unit * unit;
       if (len > max_len) return 1;
@@ -1940,13 +2096,10 @@ class StripeServer {
     auto last_check = t0;
     for (int q = 0; q < nparts && rc == 0; ++q) {
       const uint32_t *flag = &sh_->done[slot[q]][0];
-      for (unsigned spins = 0; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != want[q]; ++spins) {
-        if (spins < 500) {
-          __builtin_ia32_pause();
-          continue;
-        }
+      // spin or park (FlagWaits), checking every 100 us that the server has not retired meanwhile
+      while (!FlagWaits::get().wait(flag, want[q], std::chrono::microseconds(100))) {
         const auto now = std::chrono::steady_clock::now();
-        if (now - last_check > std::chrono::microseconds(100)) {  // did the server retire meanwhile?
+        if (now - last_check > std::chrono::microseconds(100)) {
           last_check = now;
           if ((rc = ensure_running(true))) break;
         }
@@ -1955,8 +2108,6 @@ class StripeServer {
           broken_ = true;
           break;
         }
-        if (now - t0 < std::chrono::microseconds(200)) std::this_thread::yield();
-        else std::this_thread::sleep_for(std::chrono::microseconds(20));
       }
     }
     static const bool trace = getenv("LSEC_TRACE") != nullptr;

@@ -9,7 +9,10 @@
 
 namespace lsec {
 
-constexpr int kSrvWG = 32;          // server workgroups (one per CU they land on)
+#ifndef LSEC_SRV_WG
+#define LSEC_SRV_WG 32
+#endif
+constexpr int kSrvWG = LSEC_SRV_WG;  // server workgroups (one per CU they land on)
 constexpr int kSrvSlotsPerWG = 15;  // post line word 15 is the stop word
 constexpr int kSrvSlots = kSrvWG * kSrvSlotsPerWG;
 constexpr int kSrvMaxK = 32;        // inputs of one request the server takes

@@ -24,6 +24,7 @@
  */
 #include <dlfcn.h>
 #include <pthread.h>
+#include <sys/resource.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -111,6 +112,27 @@ static int cmp(const void *a, const void *b)
     return x < y ? -1 : x > y;
 }
 
+static double cpu_seconds(void)
+{
+    struct rusage ru;
+    getrusage(RUSAGE_SELF, &ru);
+    return ru.ru_utime.tv_sec + ru.ru_stime.tv_sec + 1e-6 * (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec);
+}
+
+/* the cgroup's CPU throttling so far (cpu.stat throttled_usec; 0 without cgroup v2) */
+static double throttled_seconds(void)
+{
+    FILE *f = fopen("/sys/fs/cgroup/cpu.stat", "r");
+    char key[64];
+    long long v;
+    double t = 0;
+    if (!f) return 0;
+    while (fscanf(f, "%63s %lld", key, &v) == 2)
+        if (strcmp(key, "throttled_usec") == 0) t = v * 1e-6;
+    fclose(f);
+    return t;
+}
+
 static void run(int T, const char *impl, const char *method)
 {
     pthread_t th[1024];
@@ -125,10 +147,10 @@ static void run(int T, const char *impl, const char *method)
     }
     g_t_end = now() + 1e9;
     pthread_barrier_wait(&g_bar);  /* every thread warmed up */
-    double t0 = now();
+    double t0 = now(), c0 = cpu_seconds(), th0 = throttled_seconds();
     g_t_end = t0 + g_seconds;
     pthread_barrier_wait(&g_bar);  /* every thread done */
-    double wall = now() - t0;
+    double wall = now() - t0, cpu = cpu_seconds() - c0, thr = throttled_seconds() - th0;
     long calls = 0, n = 0;
     for (int t = 0; t < T; t++) {
         pthread_join(th[t], NULL);
@@ -150,10 +172,11 @@ static void run(int T, const char *impl, const char *method)
     printf("{\"impl\": \"%s\", \"op\": \"%s\", \"chunk\": %d, \"threads\": %d, \"calls\": %ld, \"seconds\": %.3f, "
            "\"method\": \"%s\", \"pinned\": %d, \"small_path\": \"%s\", \"per_call_us_p50\": %.1f, "
            "\"per_call_us_p99\": %.1f, \"per_call_us_p999\": %.1f, \"per_call_us_max\": %.1f, \"per_call_us_mean\": %.1f, "
-           "\"gibps\": %.3f}\n",
+           "\"gibps\": %.3f, \"cpu_util\": %.2f, \"cpu_us_per_call\": %.1f, \"cgroup_throttled_ms\": %.1f}\n",
            impl, g_decode ? "decode" : "encode", g_chunk, T, calls, wall, method, g_host_malloc != NULL, sp ? sp : "default",
            n ? lat[n / 2] * 1e6 : 0.0, n ? lat[(size_t)(n * 0.99)] * 1e6 : 0.0, n ? lat[(size_t)(n * 0.999)] * 1e6 : 0.0,
-           n ? lat[n - 1] * 1e6 : 0.0, n ? sum / n * 1e6 : 0.0, calls * (double)g_k * g_chunk / wall / (1 << 30));
+           n ? lat[n - 1] * 1e6 : 0.0, n ? sum / n * 1e6 : 0.0, calls * (double)g_k * g_chunk / wall / (1 << 30),
+           cpu / wall, calls ? cpu / calls * 1e6 : 0.0, thr * 1e3);
     fflush(stdout);
     free(lat);
 }
