@@ -274,6 +274,13 @@ struct Entry {
 
 std::mutex g_mu;
 std::condition_variable g_cv;
+int g_compiling = 0;  // compile threads still running (waited for at exit, below)
+
+// at exit: let running compiles finish (bounded) before the statics they use are destroyed
+void drain_compiles() {
+  std::unique_lock<std::mutex> lk(g_mu);
+  g_cv.wait_for(lk, std::chrono::seconds(60), [] { return g_compiling == 0; });
+}
 std::map<std::vector<uint8_t>, std::shared_ptr<Entry>> g_by_matrix;  // key: R, K, matrix
 std::map<const void *, std::shared_ptr<Entry>> g_by_image;           // device image -> entry
 
@@ -315,6 +322,7 @@ void compile(std::shared_ptr<Entry> e) {
   e->code.swap(code);
   e->err = err;
   e->state = err.empty() ? Entry::kReady : Entry::kFailed;
+  --g_compiling;
   g_cv.notify_all();
 }
 
@@ -353,6 +361,9 @@ void bind(const void *image, const uint8_t *mat, int R, int K) {
       e->K = K;
       g_by_matrix.emplace(key, e);
       start = true;
+      ++g_compiling;
+      static std::once_flag once;
+      std::call_once(once, [] { atexit(drain_compiles); });
     } else {
       e = it->second;
     }
