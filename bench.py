@@ -426,6 +426,24 @@ class HipEngine:
                 "decode_vs_probe": round((dec_hbm / t_dec) / (2 * nb / t_probe), 3)}
             del src, dst
             self.drop()
+            # the encode's own traffic mix without its arithmetic: XOR of the k data shards written
+            # to each of the m parity shards, in the encode kernel's tiles (lsec_hbm_mix_dev)
+            md = torch.empty((N, k, C), dtype=torch.uint8, device=self.dev)
+            mp = torch.empty((N, m, C), dtype=torch.uint8, device=self.dev)
+            mrefs = self.plan.shard_refs([(md.data_ptr() + j * C, k * C) for j in range(k)] +
+                                         [(mp.data_ptr() + r * C, m * C) for r in range(m)])
+
+            def mix():
+                if lib.lsec_hbm_mix_dev(mrefs, k, m, N, C, self.sh):
+                    raise E.ErasureError(E.last_error())
+
+            t_mix = timed(mix)
+            out["hbm_copy_ref"]["encode_mix"] = {
+                "what": "XOR of the k data shards to each of the m parity shards over N stripes: the encode's k:m bytes, no GF arithmetic",
+                "frac": round(enc_hbm / t_mix / HBM_PEAK, 4),
+                "encode_vs_mix": round(t_mix / t_enc, 3)}
+            del md, mp
+            self.drop()
             # the decode's own traffic mix without its arithmetic: a raid4 (k+1) decode of shard 0
             # is a plain XOR of the k survivors -- k reads : 1 write per column, as the decode
             xplan = self.L.Plan.for_chunk(E.JE_METHOD_NAMES.index("raid4"), k, 1, C)

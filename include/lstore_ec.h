@@ -233,6 +233,10 @@ void lsec_set_kernel_variant(int bytewise_variant, int bitsliced_variant);  /* t
  * (bytes a multiple of 16, 16-byte aligned device pointers) on `stream` with the coding kernels'
  * memory shape; bench.py times it as the box's practical HBM ceiling.  0 / -1. */
 int lsec_hbm_copy_dev(void *dst, const void *src, unsigned long long bytes, void *stream);
+/* Measurement probe: for every stripe, shards[k+r] <- XOR of shards[0..k) (r < m <= 16), with
+ * the RS encode kernel's tiles: the encode's k-read : m-write HBM traffic without its GF
+ * arithmetic, which bench.py times beside the encode.  0 / -1. */
+int lsec_hbm_mix_dev(const lsec_shard_t *shards, int k, int m, int nstripes, long long block_size, void *stream);
 
 #ifdef __cplusplus
 }

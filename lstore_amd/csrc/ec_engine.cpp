@@ -3348,4 +3348,21 @@ int lsec_hbm_copy_dev(void *dst, const void *src, unsigned long long bytes, void
   return 0;
 }
 
+int lsec_hbm_mix_dev(const lsec_shard_t *shards, int k, int m, int nstripes, long long block_size, void *stream) {
+  if (!shards || k < 1 || k > lsec::kMaxK || m < 1 || m > lsec::kMaxR || nstripes < 0 || block_size < 0 ||
+      block_size % 8 != 0)
+    return fail("lsec_hbm_mix_dev: bad arguments (k=%d m=%d nstripes=%d block_size=%lld)", k, m, nstripes, block_size);
+  lsec::ApplyArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.K = k;
+  a.R = m;
+  a.nstripes = nstripes;
+  a.size = block_size;
+  for (int j = 0; j < k; ++j) a.in[j] = {reinterpret_cast<uint64_t>(shards[j].base), shards[j].stride};
+  for (int r = 0; r < m; ++r) a.out[r] = {reinterpret_cast<uint64_t>(shards[k + r].base), shards[k + r].stride};
+  const hipError_t e = lsec::launch_hbm_mix(a, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return fail("lsec_hbm_mix_dev: %s", hipGetErrorString(e));
+  return 0;
+}
+
 }  // extern "C"

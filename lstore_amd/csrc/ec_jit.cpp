@@ -68,7 +68,11 @@ bool wants_xornet(int R, int K) {
     const char *s = getenv("LSEC_JIT");
     return !s || *s != '0';
   }();
-  return on && R >= 2 && R <= kMaxRows && K >= 2 && K <= kMaxCols && R * K >= 96;
+  static const int min_cells = [] {  // LSEC_JIT_MIN: smallest R * K served by a network (A/B runs)
+    const char *s = getenv("LSEC_JIT_MIN");
+    return s ? atoi(s) : 96;
+  }();
+  return on && R >= 2 && R <= kMaxRows && K >= 2 && K <= kMaxCols && R * K >= min_cells;
 }
 
 // Code shape knobs (LSEC_JIT_VARIANT, read once; A/B runs): bit 0 = common-pair elimination,

@@ -141,6 +141,9 @@ hipError_t launch_signal(unsigned *counter, unsigned *flag, unsigned value, hipS
 
 // HBM probe (measurement only): dst <- src, bytes a multiple of 16, both 16-byte aligned.
 hipError_t launch_hbm_copy(void *dst, const void *src, uint64_t bytes, hipStream_t stream);
+// HBM probe (measurement only): out[r] = XOR of the K inputs for every stripe (a.K, a.R <= kMaxR,
+// a.in / a.out / a.nstripes / a.size): the encode's K-read : R-write traffic without its arithmetic.
+hipError_t launch_hbm_mix(const ApplyArgs &a, hipStream_t stream);
 
 // Host helper: fill one cell for coefficient c.
 void make_cell(uint8_t c, CoefCell &cell);

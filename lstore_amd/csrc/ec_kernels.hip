@@ -62,7 +62,7 @@ int bytewise_variant() { return g_bw_variant; }
 hipError_t launch_bytewise(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
   if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > 8 || a.size % 8 != 0) return hipErrorInvalidValue;
   if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
-  const int shape = bytewise_shape(a.K, a.R);
+  const int shape = a.accumulate ? 1 : bytewise_shape(a.K, a.R);  // as dispatch_bytewise's accumulate launch
   const uint64_t tile = static_cast<uint64_t>(kBlock) * 4 * bw_shape_vw(shape) * bw_shape_it(shape);
   const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
@@ -85,7 +85,7 @@ hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid_blocks)
       a.size % (8LL * a.packet) != 0)
     return hipErrorInvalidValue;
   if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
-  int dw = (g_bs_variant == 2 || g_bs_variant == 4) && !a.magic_acc ? g_bs_variant : 1;
+  int dw = (g_bs_variant == 2 || g_bs_variant == 4) && !a.magic_acc && !a.accumulate ? g_bs_variant : 1;
   while (dw > 1 && a.packet % (4 * dw) != 0) dw >>= 1;
   const uint64_t col_bytes = a.size / 8;
   const uint64_t tile = kBlock * 4ull * dw;
@@ -258,6 +258,51 @@ __global__ __launch_bounds__(kBlock) void k_hbm_copy(uint64_t dst, uint64_t src,
   }
 }
 
+// The encode's own traffic shape with no arithmetic (measurement probe): per stripe, the XOR of
+// K input shards written to each of R output shards, in the RS encode kernel's tiles (2 x 16 B
+// per lane, one 8 KiB column tile per block, XCD-contiguous tile order, non-temporal loads and
+// stores) -- so K reads : R writes per column, as the encode.
+__global__ __launch_bounds__(kBlock) void k_hbm_mix(ApplyArgs a) {
+  constexpr int kIt = 2, kTile = kBlock * 16 * kIt;
+  const int64_t C = a.size;
+  const uint32_t tps = static_cast<uint32_t>((C + kTile - 1) / kTile);
+  const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
+  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+    const uint32_t s = t / tps;
+    const int64_t off0 = static_cast<int64_t>(t - s * tps) * kTile + threadIdx.x * 16;
+    u32x4 acc[kIt] = {0u, 0u};
+    for (int j = 0; j < a.K; ++j) {
+      const uint64_t p = a.in[j].base + s * a.in[j].stride;
+#pragma unroll
+      for (int it = 0; it < kIt; ++it) {
+        const int64_t o = off0 + it * kBlock * 16;
+        if (o + 16 <= C) {
+          acc[it] ^= __builtin_nontemporal_load(gptr<u32x4>(p + o));
+        } else if (o < C) {
+          const u32x2 h = *gptr<u32x2>(p + o);
+          acc[it].x ^= h.x;
+          acc[it].y ^= h.y;
+        }
+      }
+    }
+    for (int r = 0; r < a.R; ++r) {
+      const uint64_t q = a.out[r].base + s * a.out[r].stride;
+#pragma unroll
+      for (int it = 0; it < kIt; ++it) {
+        const int64_t o = off0 + it * kBlock * 16;
+        if (o + 16 <= C) {
+          __builtin_nontemporal_store(acc[it], gptr_w<u32x4>(q + o));
+        } else if (o < C) {
+          u32x2 h;
+          h.x = acc[it].x;
+          h.y = acc[it].y;
+          *gptr_w<u32x2>(q + o) = h;
+        }
+      }
+    }
+  }
+}
+
 // A small grid striding over the pieces, every lane holding its 4 x 16 B of a piece in flight
 // before storing: enough bytes in flight for PCIe, while the H2D and D2H launches (on two
 // streams) and the coding kernel between them all keep room on the CUs.  (One block per piece
@@ -323,6 +368,16 @@ hipError_t launch_hbm_copy(void *dst, const void *src, uint64_t bytes, hipStream
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_hbm_copy, dim3(default_grid(ntiles)), dim3(kBlock), 0, st, reinterpret_cast<uint64_t>(dst),
                      reinterpret_cast<uint64_t>(src), n16);
+  return hipGetLastError();
+}
+
+hipError_t launch_hbm_mix(const ApplyArgs &a, hipStream_t st) {
+  if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > kMaxR || a.size % 8 != 0) return hipErrorInvalidValue;
+  if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
+  const uint64_t tile = kBlock * 16 * 2;
+  const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
+  if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_hbm_mix, dim3(default_grid(ntiles)), dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
 

@@ -63,16 +63,18 @@ __device__ __forceinline__ LSEC_GLOBAL T *gptr_w(uint64_t addr) {
   return reinterpret_cast<LSEC_GLOBAL T *>(addr);
 }
 
-// Output stores.  ApplyArgs::accumulate (wave-uniform) XORs the result into what the output
-// holds: the second and later input groups of a stripe wider than kMaxK inputs.
-template <typename V>
-__device__ __forceinline__ void put_nt(int accumulate, uint64_t q, V v) {
-  if (accumulate) v ^= *gptr<V>(q);
+// Output stores.  ACC XORs the result into what the output holds: the second and later input
+// groups of a stripe wider than kMaxK inputs (ApplyArgs::accumulate), launched on separate
+// ACC instantiations -- a run-time branch at the stores cost the hot kernels registers (RS
+// 10+4: 155 -> 268 VGPRs, occupancy 3 -> 1, 0.77 -> 0.55 of 8 TB/s).
+template <bool ACC, typename V>
+__device__ __forceinline__ void put_nt(uint64_t q, V v) {
+  if constexpr (ACC) v ^= *gptr<V>(q);
   __builtin_nontemporal_store(v, gptr_w<V>(q));
 }
-template <typename V>
-__device__ __forceinline__ void put(int accumulate, uint64_t q, V v) {
-  if (accumulate) v ^= *gptr<V>(q);
+template <bool ACC, typename V>
+__device__ __forceinline__ void put(uint64_t q, V v) {
+  if constexpr (ACC) v ^= *gptr<V>(q);
   *gptr_w<V>(q) = v;
 }
 
@@ -309,7 +311,7 @@ __device__ __forceinline__ void bw_magic_out(MagicLane &ml, int K, const typenam
 // BF = branch-free coefficient path (bw_accumulate_bf).
 // MG = also accumulate the stripe magic of inputs + outputs (encode + je_cksum_calc fused).
 // X0 = row 0 is a plain XOR (see bw_accumulate_bf).
-template <int R, int KC, int IT, bool BF, int VW, bool MG, bool X0>
+template <int R, int KC, int IT, bool BF, int VW, bool MG, bool X0, bool ACC>
 __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
   typedef typename VecT<VW>::type V;
   __shared__ uint32_t red[MG ? kBlock / 64 : 1];
@@ -381,7 +383,7 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
       for (int r = 0; r < R; ++r) {
         const uint64_t q = a.out[r].base + s * a.out[r].stride + off0;
 #pragma unroll
-        for (int it = 0; it < IT; ++it) put_nt<V>(a.accumulate, q + it * kStep, acc[it][r]);
+        for (int it = 0; it < IT; ++it) put_nt<ACC, V>(q + it * kStep, acc[it][r]);
       }
     } else {
       // ragged last tile: C is a multiple of 8, so a 16-byte lane unit may be half full
@@ -413,12 +415,12 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
         for (int it = 0; it < IT; ++it) {
           const int64_t o = off0 + it * kStep;
           if (o + kLane <= C) {
-            put<V>(a.accumulate, q + o, acc[it][r]);
+            put<ACC, V>(q + o, acc[it][r]);
           } else if (o < C) {
             u32x2 h;
             h.x = acc[it][r][0];
             h.y = acc[it][r][1];
-            put<u32x2>(a.accumulate, q + o, h);
+            put<ACC, u32x2>(q + o, h);
           }
         }
       }
@@ -434,22 +436,22 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
 // instantiations once per wave: a uniform branch outside the tile loop, no merges inside it.
 // Only codes with K*R >= 40 cells take the dual form: narrow codes are HBM-bound, and the
 // second path would only raise the kernel's register allocation (RS 6+3: 56 -> 108 VGPRs).
-template <int R, int KC, int IT, bool BF, int VW, bool MG = false>
+template <int R, int KC, int IT, bool BF, int VW, bool MG = false, bool ACC = false>
 __global__ __launch_bounds__(kBlock) void k_gf8_bytewise(ApplyArgs a) {
   if constexpr (BF && R >= 2 && (KC == 0 || KC * R >= 40)) {
     if (const_cells(a.cells)->pad & kCellXorRow) {
-      bytewise_tiles<R, KC, IT, BF, VW, MG, true>(a);
+      bytewise_tiles<R, KC, IT, BF, VW, MG, true, ACC>(a);
       return;
     }
   }
-  bytewise_tiles<R, KC, IT, BF, VW, MG, false>(a);
+  bytewise_tiles<R, KC, IT, BF, VW, MG, false, ACC>(a);
 }
 
 // ------------------------------------------------------------------ bitsliced
 // A lane owns DW consecutive dwords of packet-column space in one super-packet and reads
 // the same columns of all 8 packets of every input shard.  MG: also the stripe magic of the
 // inputs and outputs (encode + je_cksum_calc in one pass, as the bytewise kernel does).
-template <int R, int KC, int DW, bool MG = false>
+template <int R, int KC, int DW, bool MG = false, bool ACC = false>
 __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
   typedef typename VecT<DW>::type V;
   __shared__ uint32_t red[MG ? kBlock / 64 : 1];
@@ -518,7 +520,7 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
       for (int r = 0; r < R; ++r) {
         const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
 #pragma unroll
-        for (int x = 0; x < 8; ++x) put_nt<V>(a.accumulate, q + x * P, acc[r][x]);
+        for (int x = 0; x < 8; ++x) put_nt<ACC, V>(q + x * P, acc[r][x]);
         if constexpr (MG) ml_add<8, DW>(ml, acc[r], static_cast<uint32_t>(K + r));
       }
     }
@@ -575,7 +577,7 @@ __global__ __launch_bounds__(kBlock) void k_bitmatrix(ApplyArgs a) {
     for (int r = 0; r < R; ++r) {
       const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
 #pragma unroll
-      for (int l = 0; l < W; ++l) put_nt<uint32_t>(a.accumulate, q + l * P, acc[r][l]);
+      for (int l = 0; l < W; ++l) put_nt<false, uint32_t>(q + l * P, acc[r][l]);
     }
   }
 }
@@ -645,7 +647,8 @@ __global__ __launch_bounds__(kBlock) void k_bitmatrix_any(ApplyArgs a) {
 #pragma unroll
           for (int l = 0; l < kChunk; ++l) {
             if (l >= nl) continue;
-            put_nt<uint32_t>(a.accumulate, q + static_cast<uint64_t>(l0 + l) * P, acc[r][l]);
+            if (a.accumulate) put_nt<true, uint32_t>(q + static_cast<uint64_t>(l0 + l) * P, acc[r][l]);
+            else put_nt<false, uint32_t>(q + static_cast<uint64_t>(l0 + l) * P, acc[r][l]);
           }
         }
       }
@@ -676,7 +679,7 @@ __device__ __forceinline__ uint32_t bit_smear(uint32_t x, int b) {
   }
 }
 
-template <int R, int W>
+template <int R, int W, bool ACC = false>
 __global__ __launch_bounds__(kBlock) void k_gfw_wordwise(ApplyArgs a) {
   constexpr int VW = W == 16 ? 4 : 2;
   typedef typename VecT<VW>::type V;
@@ -732,12 +735,12 @@ __global__ __launch_bounds__(kBlock) void k_gfw_wordwise(ApplyArgs a) {
     for (int r = 0; r < R; ++r) {
       const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
       if (whole) {
-        put_nt<V>(a.accumulate, q, acc[r]);
+        put_nt<ACC, V>(q, acc[r]);
       } else {
         u32x2 h;
         h.x = acc[r][0];
         h.y = acc[r][1];
-        put<u32x2>(a.accumulate, q, h);
+        put<ACC, u32x2>(q, h);
       }
     }
   }
@@ -770,7 +773,7 @@ __device__ __forceinline__ void times_x_sliced(uint32_t (&e)[W]) {
   }
 }
 
-template <int R, int W>
+template <int R, int W, bool ACC = false>
 __global__ __launch_bounds__(kBlock) void k_gfw_bitsliced(ApplyArgs a) {
   const int K = a.K;
   const uint32_t P = static_cast<uint32_t>(a.packet);
@@ -818,7 +821,7 @@ __global__ __launch_bounds__(kBlock) void k_gfw_bitsliced(ApplyArgs a) {
     for (int r = 0; r < R; ++r) {
       const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
 #pragma unroll
-      for (int l = 0; l < W; ++l) put_nt<uint32_t>(a.accumulate, q + l * P, acc[r][l]);
+      for (int l = 0; l < W; ++l) put_nt<ACC, uint32_t>(q + l * P, acc[r][l]);
     }
   }
 }
@@ -864,7 +867,7 @@ __device__ __forceinline__ void transpose_units(uint32_t (&D)[W]) {
   transpose_bits<W, 1>(D, 0x55555555u);
 }
 
-template <int R, int W, bool xor_only>
+template <int R, int W, bool xor_only, bool ACC>
 __device__ __forceinline__ void gfw_transposed_tiles(const ApplyArgs &a) {
   constexpr int kPieces = W / 4;  // 16 B pieces per lane per shard
   constexpr uint32_t kTile = kBlock * 4 * W;
@@ -941,12 +944,12 @@ __device__ __forceinline__ void gfw_transposed_tiles(const ApplyArgs &a) {
         const int64_t o = base + static_cast<int64_t>(q) * kBlock * 16;
         const u32x4 v = {acc[r][4 * q], acc[r][4 * q + 1], acc[r][4 * q + 2], acc[r][4 * q + 3]};
         if (whole || o + 16 <= C) {
-          put_nt<u32x4>(a.accumulate, q0 + o, v);
+          put_nt<ACC, u32x4>(q0 + o, v);
         } else if (o + 8 <= C) {
           u32x2 h;
           h.x = v.x;
           h.y = v.y;
-          put<u32x2>(a.accumulate, q0 + o, h);
+          put<ACC, u32x2>(q0 + o, h);
         }
       }
     }
@@ -955,16 +958,16 @@ __device__ __forceinline__ void gfw_transposed_tiles(const ApplyArgs &a) {
 
 // One kernel, two whole tile loops chosen by a uniform branch: a launch whose coefficients are
 // all 0 / 1 (XOR-of-survivors decodes) is plain XOR and skips the bit slicing.
-template <int R, int W>
+template <int R, int W, bool ACC = false>
 __global__ __launch_bounds__(kBlock) void k_gfw_transposed(ApplyArgs a) {
   constexpr uint32_t kCoefMask = W == 16 ? 0xFFFFu : 0xFFFFFFFFu;
   ConstU32 *prod = reinterpret_cast<ConstU32 *>(reinterpret_cast<uintptr_t>(a.masks));
   bool xor_only = true;
   for (int i = 0; i < R * a.K && xor_only; ++i) xor_only = (prod[i * W] & kCoefMask) <= 1u;
   if (xor_only)
-    gfw_transposed_tiles<R, W, true>(a);
+    gfw_transposed_tiles<R, W, true, ACC>(a);
   else
-    gfw_transposed_tiles<R, W, false>(a);
+    gfw_transposed_tiles<R, W, false, ACC>(a);
 }
 
 // word sizes the liberation family can produce: primes (liberation), p-1 for prime p
@@ -996,6 +999,10 @@ inline int bw_shape_vw(int shape) { return shape <= 1 ? 4 : 2; }
 
 template <int R>
 hipError_t dispatch_bytewise(const ApplyArgs &a, hipStream_t st, int grid, int shape) {
+  if (a.accumulate) {  // a later input group of a wide stripe: generic K, 16 B per lane (shape 1)
+    hipLaunchKernelGGL((k_gf8_bytewise<R, 0, 1, true, 4, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
+    return hipGetLastError();
+  }
   switch (shape) {
     case 1: return bytewise_k<R, 1, true, 4>(a, st, grid);
     case 2: return bytewise_k<R, 2, true, 2>(a, st, grid);
@@ -1028,6 +1035,10 @@ hipError_t dispatch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid, int 
     hipLaunchKernelGGL((k_gf8_bitsliced<R, 0, 1, true>), dim3(grid), dim3(kBlock), 0, st, a);
     return hipGetLastError();
   }
+  if (a.accumulate) {  // a later input group of a wide stripe, one lane dword wide
+    hipLaunchKernelGGL((k_gf8_bitsliced<R, 0, 1, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
+    return hipGetLastError();
+  }
   switch (dw) {
     case 4: hipLaunchKernelGGL((k_gf8_bitsliced<R, 0, 4>), dim3(grid), dim3(kBlock), 0, st, a); break;
     case 2: hipLaunchKernelGGL((k_gf8_bitsliced<R, 0, 2>), dim3(grid), dim3(kBlock), 0, st, a); break;
@@ -1039,6 +1050,10 @@ hipError_t dispatch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid, int 
 template <int R>
 hipError_t dispatch_bitmatrix(const ApplyArgs &a, hipStream_t st, int grid) {
   if constexpr (R <= 2) {
+    if (a.accumulate) {  // wide stripes (k > 64) only occur at w > 64: the any-w kernel
+      hipLaunchKernelGGL((k_bitmatrix_any<R>), dim3(grid), dim3(kBlock), 0, st, a);
+      return hipGetLastError();
+    }
     switch (a.w) {
 #define LSEC_BM_W(WW) \
   case WW: hipLaunchKernelGGL((k_bitmatrix<R, WW>), dim3(grid), dim3(kBlock), 0, st, a); break;
@@ -1054,9 +1069,11 @@ hipError_t dispatch_bitmatrix(const ApplyArgs &a, hipStream_t st, int grid) {
 
 template <int R>
 hipError_t dispatch_wordwise(const ApplyArgs &a, hipStream_t st, int grid) {
-  switch (a.w) {
-    case 16: hipLaunchKernelGGL((k_gfw_wordwise<R, 16>), dim3(grid), dim3(kBlock), 0, st, a); break;
-    case 32: hipLaunchKernelGGL((k_gfw_wordwise<R, 32>), dim3(grid), dim3(kBlock), 0, st, a); break;
+  switch (a.w * 2 + (a.accumulate ? 1 : 0)) {
+    case 32: hipLaunchKernelGGL((k_gfw_wordwise<R, 16>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    case 33: hipLaunchKernelGGL((k_gfw_wordwise<R, 16, true>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    case 64: hipLaunchKernelGGL((k_gfw_wordwise<R, 32>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    case 65: hipLaunchKernelGGL((k_gfw_wordwise<R, 32, true>), dim3(grid), dim3(kBlock), 0, st, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -1066,10 +1083,12 @@ hipError_t dispatch_wordwise(const ApplyArgs &a, hipStream_t st, int grid) {
 template <int R>
 hipError_t dispatch_gfw_transposed(const ApplyArgs &a, hipStream_t st, int grid) {
   if (a.w == 16) {
-    hipLaunchKernelGGL((k_gfw_transposed<R, 16>), dim3(grid), dim3(kBlock), 0, st, a);
+    if (a.accumulate) hipLaunchKernelGGL((k_gfw_transposed<R, 16, true>), dim3(grid), dim3(kBlock), 0, st, a);
+    else hipLaunchKernelGGL((k_gfw_transposed<R, 16>), dim3(grid), dim3(kBlock), 0, st, a);
   } else if constexpr (R <= 4) {
     if (a.w != 32) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_gfw_transposed<R, 32>), dim3(grid), dim3(kBlock), 0, st, a);
+    if (a.accumulate) hipLaunchKernelGGL((k_gfw_transposed<R, 32, true>), dim3(grid), dim3(kBlock), 0, st, a);
+    else hipLaunchKernelGGL((k_gfw_transposed<R, 32>), dim3(grid), dim3(kBlock), 0, st, a);
   } else {
     return hipErrorInvalidValue;
   }
@@ -1079,10 +1098,12 @@ hipError_t dispatch_gfw_transposed(const ApplyArgs &a, hipStream_t st, int grid)
 template <int R>
 hipError_t dispatch_gfw_bitsliced(const ApplyArgs &a, hipStream_t st, int grid) {
   if (a.w == 16) {
-    hipLaunchKernelGGL((k_gfw_bitsliced<R, 16>), dim3(grid), dim3(kBlock), 0, st, a);
+    if (a.accumulate) hipLaunchKernelGGL((k_gfw_bitsliced<R, 16, true>), dim3(grid), dim3(kBlock), 0, st, a);
+    else hipLaunchKernelGGL((k_gfw_bitsliced<R, 16>), dim3(grid), dim3(kBlock), 0, st, a);
   } else if constexpr (R <= 4) {
     if (a.w != 32) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_gfw_bitsliced<R, 32>), dim3(grid), dim3(kBlock), 0, st, a);
+    if (a.accumulate) hipLaunchKernelGGL((k_gfw_bitsliced<R, 32, true>), dim3(grid), dim3(kBlock), 0, st, a);
+    else hipLaunchKernelGGL((k_gfw_bitsliced<R, 32>), dim3(grid), dim3(kBlock), 0, st, a);
   } else {
     return hipErrorInvalidValue;
   }

@@ -78,7 +78,7 @@ EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan",
            "lsec_decode_dev", "et_encode_stripes_magic", "et_stripes_magic", "lsec_encode_magic_dev",
            "lsec_stripe_magic_dev", "lsec_segment_write", "lsec_segment_write_iov", "lsec_segment_read", "lsec_segment_inspect",
            "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count", "lsec_last_error", "lsec_plan_kernel",
-           "lsec_set_kernel_variant", "lsec_set_host_devices", "lsec_hbm_copy_dev", "lsec_prepare_encode", "lsec_plan_jit")
+           "lsec_set_kernel_variant", "lsec_set_host_devices", "lsec_hbm_copy_dev", "lsec_hbm_mix_dev", "lsec_prepare_encode", "lsec_plan_jit")
 
 # read / inspect flags and stripe states (include/lstore_ec.h)
 READ_PARANOID, MAGIC_LEGACY, INSPECT_FIX, MAX_DEVS = 1, 2, 4, 256
@@ -150,6 +150,7 @@ def lib():
     L.lsec_set_kernel_variant.restype = None
     L.lsec_set_host_devices.argtypes = [C.POINTER(C.c_int), C.c_int]
     L.lsec_hbm_copy_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_ulonglong, C.c_void_p]
+    L.lsec_hbm_mix_dev.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_void_p]
     _lib = L
     return L
 

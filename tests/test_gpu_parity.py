@@ -814,6 +814,29 @@ def test_hbm_copy_probe(cuda):
     assert lib.lsec_hbm_copy_dev(buf.data_ptr() + 8, buf.data_ptr() + 32, 16, st) == -1
 
 
+def test_hbm_mix_probe(cuda):
+    """lsec_hbm_mix_dev (bench.py's encode-traffic probe) writes the XOR of the k inputs to each
+    of the m outputs of every stripe, ragged tails included, and refuses bad arguments."""
+    import torch
+
+    from lstore_amd import erasure as E
+
+    lib = E.lib()
+    st = torch.cuda.current_stream().cuda_stream
+    for k, m, C, N in ((6, 3, 8192 + 24, 5), (10, 4, 65536, 3), (1, 1, 8, 2)):
+        d = torch.randint(0, 256, (N, k, C), dtype=torch.uint8, device=cuda)
+        p = torch.zeros((N, m, C), dtype=torch.uint8, device=cuda)
+        refs = [(d.data_ptr() + j * C, k * C) for j in range(k)] + [(p.data_ptr() + r * C, m * C) for r in range(m)]
+        arr = L.Plan.shard_refs(refs)
+        assert lib.lsec_hbm_mix_dev(arr, k, m, N, C, st) == 0
+        torch.cuda.synchronize()
+        x = np.bitwise_xor.reduce(d.cpu().numpy(), axis=1)
+        for r in range(m):
+            assert np.array_equal(p[:, r].cpu().numpy(), x)
+    assert lib.lsec_hbm_mix_dev(arr, 0, 1, 1, 8, st) == -1
+    assert lib.lsec_hbm_mix_dev(arr, 1, 1, 1, 12, st) == -1
+
+
 # ---------------------------------------------------------------- SURVEY §8d c2 correctness patterns
 def _special_stripes(k, size, P):
     """All-zero, all-0xFF and single-bit stripes: stripe 2 + j*8 + t has only bit t of one byte

@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--variants", default="0,0;1,0;0,2;0,4")
     ap.add_argument("--magic", action="store_true", help="also time fused encode+magic and standalone magic")
     ap.add_argument("--pad", type=int, default=0, help="bytes of padding after every shard (HBM channel spread)")
+    ap.add_argument("--mix", action="store_true",
+                    help="also time lsec_hbm_mix_dev over the same shards: the encode's traffic, XOR only")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     variants = [tuple(int(x) for x in v.split(",")) for v in a.variants.split(";")]
@@ -63,7 +65,24 @@ def main():
         ref_par = par.clone()
         stream = torch.cuda.current_stream()
         res = {v: ([], []) for v in variants}
+        tmix = []
+        if a.mix:
+            lib = E.lib()
+            mrefs = L.Plan.shard_refs(plan.tensor_refs(data, par)[0])
+
+            def mix():
+                assert lib.lsec_hbm_mix_dev(mrefs, k, m, N, C, stream.cuda_stream) == 0
         for _ in range(a.rounds):
+            if a.mix:
+                mix()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(a.reps):
+                    mix()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                tmix.append(e0.elapsed_time(e1) / a.reps)
+                plan.encode_dev(data, par)  # restore the parity the variants are checked against
             for v in variants:
                 E.set_kernel_variant(*v)
                 e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
@@ -87,6 +106,11 @@ def main():
             db = (k + 1) * C * N
             print(f"{name:6s} N={N:5d} variant={v} jit={int(plan.jit()) if v == (0, 0) else 0}  encode {te:8.3f} ms {eb / te / 1e6:7.1f} GB/s "
                   f"({eb / te / 8e9:5.1%})   decode {td:8.3f} ms {db / td / 1e6:7.1f} GB/s ({db / td / 8e9:5.1%})",
+                  flush=True)
+        if tmix:
+            tm = sorted(tmix)[len(tmix) // 2]
+            eb = (k + m) * C * N
+            print(f"{name:6s} N={N:5d} mix probe (XOR of k to m, no GF)  {tm:8.3f} ms {eb / tm / 1e6:7.1f} GB/s ({eb / tm / 8e9:5.1%})",
                   flush=True)
         E.set_kernel_variant(0, 0)
         if a.magic:
