@@ -327,6 +327,13 @@ class HipEngine:
 
         return encode, decode
 
+    def random_bytes(self, shape, seed=4321):
+        """probe inputs: seeded random bytes like the coding kernels' stripes (HBM rates depend
+        on the bytes moved, so a probe over zero pages would not be the same traffic)"""
+        torch = self.torch
+        g = torch.Generator(device=self.dev).manual_seed(seed)
+        return torch.randint(0, 256, shape, dtype=torch.uint8, device=self.dev, generator=g)
+
     def drop(self):
         self.tensors = None
         self.torch.cuda.empty_cache()
@@ -400,7 +407,7 @@ class HipEngine:
             # encode launch's byte count (half read, half written), HIP events on the launch stream --
             # the engine's probe kernel (lsec_hbm_copy_dev: the coding kernels' memory shape) and torch's copy_
             nb = enc_hbm // 2
-            src = torch.empty(nb, dtype=torch.uint8, device=self.dev)
+            src = self.random_bytes((nb,))
             dst = torch.empty_like(src)
 
             def probe():
@@ -428,7 +435,7 @@ class HipEngine:
             self.drop()
             # the encode's own traffic mix without its arithmetic: XOR of the k data shards written
             # to each of the m parity shards, in the encode kernel's tiles (lsec_hbm_mix_dev)
-            md = torch.empty((N, k, C), dtype=torch.uint8, device=self.dev)
+            md = self.random_bytes((N, k, C))
             mp = torch.empty((N, m, C), dtype=torch.uint8, device=self.dev)
             mrefs = self.plan.shard_refs([(md.data_ptr() + j * C, k * C) for j in range(k)] +
                                          [(mp.data_ptr() + r * C, m * C) for r in range(m)])
@@ -447,7 +454,7 @@ class HipEngine:
             # the decode's own traffic mix without its arithmetic: a raid4 (k+1) decode of shard 0
             # is a plain XOR of the k survivors -- k reads : 1 write per column, as the decode
             xplan = self.L.Plan.for_chunk(E.JE_METHOD_NAMES.index("raid4"), k, 1, C)
-            xd = torch.empty((N, k, C), dtype=torch.uint8, device=self.dev)
+            xd = self.random_bytes((N, k, C))
             xp = torch.empty((N, 1, C), dtype=torch.uint8, device=self.dev)
             refs, n, size = xplan.tensor_refs(xd, xp)
             t_xor = timed(lambda: xplan.decode_dev_refs(refs, n, size, [0], self.sh))
