@@ -927,10 +927,14 @@ class InPlacePin {
     size_t total = 0;
     for (const auto &r : regions) total += static_cast<size_t>(r.second - r.first);
     if (total < kMinBytes) return false;  // packing a small batch is cheaper than the syscalls
-    // Each DMA from registered pageable memory costs ~50 us on top of the bytes (measured:
-    // 1 MB runs move at 14 GiB/s, 40 MB runs at 48), so pin only when the copies the pinned
-    // path will issue (one per run of host-contiguous chunks, stripe by stripe) average
-    // >= 4 MiB; smaller runs pack faster (profiles/r01_v20_sweep_c5.jsonl).
+    // Each DMA from registered pageable memory has a fixed cost on top of the bytes, so pin
+    // only when the copies the pinned path will issue (one per run of host-contiguous chunks,
+    // stripe by stripe) average >= 768 KiB; smaller runs pack faster.  Measured A/B of the
+    // threshold (tools/pin_run_ab.py, profiles/r02_v27_pin_run_ab.jsonl): runs of 896 KiB and
+    // up pin faster (RS(6+3) C = 256 KiB decode 30 -> 35 GiB/s, C = 512 KiB 28 -> 41, C = 1 MiB
+    // decode 31 -> 46; RS(10+4) C = 128 KiB encode 29 -> 31), 704 KiB ties and 576 KiB and
+    // below pack faster (RS(6+3) C = 64 KiB encode 26 vs 17).  Round 1's 4 MiB threshold had
+    // every decode below C = 2 MiB packing.
     size_t runs = 0;
     for (const std::vector<int> *ids : {&in_ids, &out_ids}) {
       const char *end = nullptr;
@@ -942,7 +946,7 @@ class InPlacePin {
         }
     }
     if (runs == 0) return false;
-    small_runs_ = total / runs < kMinRun;
+    small_runs_ = total / runs < min_run();
     if (small_runs_ && !kernel_ok) return false;
     {
       // claim the page-rounded regions, so a concurrent call over the same pages packs
@@ -1006,7 +1010,12 @@ class InPlacePin {
  private:
   static constexpr size_t kMaxRegions = 1024;
   static constexpr size_t kMinBytes = 8ull << 20;
-  static constexpr size_t kMinRun = 4ull << 20;
+  static constexpr size_t kMinRun = 768ull << 10;
+  // LSEC_PIN_MIN_RUN_KB overrides kMinRun (read per call: measurement A/B runs)
+  static size_t min_run() {
+    const char *s = getenv("LSEC_PIN_MIN_RUN_KB");
+    return s && *s ? static_cast<size_t>(strtoull(s, nullptr, 10)) << 10 : kMinRun;
+  }
   struct Alias {
     const char *lo, *hi;
     intptr_t delta;
