@@ -13,14 +13,18 @@
 // HIP kernels in ec_kernels.hip.  If the GPU is unavailable the calls fail (status -1, or
 // abort() from the void encode_block fn-pointer).
 #include <hip/hip_runtime.h>
+#include <linux/futex.h>
 #include <sched.h>
 #include <strings.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdarg>
+#include <climits>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -1788,6 +1792,18 @@ size_t zerocopy_limit() {  // per-call bytes (inputs + outputs) served this way;
   return b;
 }
 
+// Completion signals of zero-copy calls (flag in coherent page-locked memory, arrival counter
+// in device memory) are pooled per device and never freed: a poller (FlagWaits) may read a flag
+// just as the thread that owned it exits.
+struct SignalBlock {
+  unsigned *flag, *dflag, *counter;
+};
+std::mutex g_signal_mu;
+std::map<int, std::vector<SignalBlock>> &signal_pool() {
+  static auto *p = new std::map<int, std::vector<SignalBlock>>();  // leaked with the blocks
+  return *p;
+}
+
 struct ZcSlot {  // one calling thread's page-locked slot on one device
   char *h = nullptr;
   uint64_t d = 0;  // its device address
@@ -1796,16 +1812,33 @@ struct ZcSlot {  // one calling thread's page-locked slot on one device
   // kernel's arrival counter in device memory, and the value the next call waits for
   unsigned *flag = nullptr, *dflag = nullptr, *counter = nullptr;
   unsigned seq = 0;
+  int dev = -1;
+  bool clean = true;  // every signal launched was seen: the block can serve another thread
   ZcSlot() = default;
   ZcSlot(const ZcSlot &) = delete;
   ZcSlot &operator=(const ZcSlot &) = delete;
   ~ZcSlot() {
     if (h) (void)hipHostFree(h);
-    if (flag) (void)hipHostFree(flag);
-    if (counter) (void)hipFree(counter);
+    if (flag && clean) {
+      std::lock_guard<std::mutex> lk(g_signal_mu);
+      signal_pool()[dev].push_back({flag, dflag, counter});
+    }
   }
   int init_signal() {
     if (flag) return 0;
+    HIP_OK(hipGetDevice(&dev));
+    {
+      std::lock_guard<std::mutex> lk(g_signal_mu);
+      std::vector<SignalBlock> &pool = signal_pool()[dev];
+      if (!pool.empty()) {
+        flag = pool.back().flag;
+        dflag = pool.back().dflag;
+        counter = pool.back().counter;
+        pool.pop_back();
+        seq = __atomic_load_n(flag, __ATOMIC_ACQUIRE);  // continue the sequence the flag holds
+        return 0;
+      }
+    }
     HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&flag), 64, hipHostMallocCoherent));
     *flag = 0;
     void *d = nullptr;
@@ -1828,7 +1861,7 @@ int zc_complete(ZcSlot &sl, hipStream_t st) {
   const hipError_t e = lsec::launch_signal(sl.counter, sl.dflag, v, st);
   if (e != hipSuccess) return fail("signal launch: %s", hipGetErrorString(e));
   int rc = 0;
-  wait_flag(sl.flag, v, st, &rc);
+  if (!wait_flag(sl.flag, v, st, &rc)) sl.clean = false;
   return rc;
 }
 
@@ -1867,23 +1900,40 @@ int usable_cpus() {
 // Completion waits.  LStore calls encode_block from up to 300 pool threads; a waiter that spins
 // (or yields) holds a CPU, and with more waiters than CPUs the spinning starves the threads whose
 // calls are done -- on a cgroup quota it also burns the quota and gets the whole process
-// throttled.  So at most half the usable CPUs spin; every other waiter parks on its own
-// condition variable, and one poller thread watches the parked waiters' flags and wakes them.
+// throttled.  So at most a quarter of the usable CPUs spin; every other waiter parks on a futex
+// word of its own, and poller threads watch the parked waiters' flags (written by the GPU, which
+// cannot wake a thread) and wake them.
+//
+// Parking is lock-free: each thread owns a record in a static table (its flags and wanted values
+// copied in, published under a sequence lock), and the pollers scan the table.  An earlier form
+// (one poller holding one mutex over a list of condition variables while it scanned and
+// notified) capped per-stripe calls at ~150k/s: at 32 and 128 threads an RS(6+3) 16 KiB encode
+// ran 12.5-13.7 GiB/s against 20.9 at 8 threads, with CPUs to spare
+// (profiles/r02_v28_zc_routes.txt).  Every flag a record can name stays mapped for the life of
+// the process (server done lines; zero-copy flags come from a pool that is never freed), so a
+// poller that reads a record just as its waiter leaves reads valid memory.
 class FlagWaits {
  public:
+  static constexpr int kMaxFlags = 16;  // flags one wait covers (StripeServer::kMaxParts)
+
   static FlagWaits &get() {
-    static FlagWaits *w = new FlagWaits();  // leaked: the poller thread outlives static destruction
+    static FlagWaits *w = new FlagWaits();  // leaked: the poller threads outlive static destruction
     return *w;
   }
 
-  // Waits until *flag reaches want (wrapping u32 sequence: want - *flag <= 0), or up to `slice`;
-  // true when reached.  Callers loop, doing their own checks between slices.
-  bool wait(const unsigned *flag, unsigned want, std::chrono::microseconds slice) {
-    if (reached(flag, want)) return true;
-    if (spin_only_) {  // LSEC_WAIT=spin (A/B runs): every waiter spins, then yields, then naps
+  // Waits until every flags[i] reaches wants[i] (wrapping u32 sequences: wants[i] - *flags[i] <= 0),
+  // or up to `slice`; true when all are reached.  Callers loop, doing their own checks between
+  // slices.  One wait covers all the parts of a call: the parts land on different server
+  // workgroups and finish in any order (a wait per part could park and wake its thread once
+  // per part under load).
+  bool wait(const unsigned *const *flags, const unsigned *wants, int n, std::chrono::microseconds slice) {
+    int from = 0;
+    if (reached_all(flags, wants, n, from)) return true;
+    Record *rec = n <= kMaxFlags ? my_record() : nullptr;
+    if (spin_only_ || !rec) {  // LSEC_WAIT=spin (A/B runs), or no record: spin, then yield, then nap
       const auto t0 = std::chrono::steady_clock::now();
       for (unsigned i = 0;; ++i) {
-        if (reached(flag, want)) return true;
+        if (reached_all(flags, wants, n, from)) return true;
         if (i < 500) {
           __builtin_ia32_pause();
           continue;
@@ -1901,7 +1951,7 @@ class FlagWaits {
     const int active = spinners_.fetch_add(1, std::memory_order_relaxed) + 1;
     if (short_waits && active <= spin_limit_) {
       for (unsigned i = 1;; ++i) {
-        if (reached(flag, want)) {
+        if (reached_all(flags, wants, n, from)) {
           spinners_.fetch_sub(1, std::memory_order_relaxed);
           note(t0);
           return true;
@@ -1911,35 +1961,88 @@ class FlagWaits {
       }
     }
     spinners_.fetch_sub(1, std::memory_order_relaxed);
-    Parked pk{flag, want};
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      parked_.push_back(&pk);
+    // park: publish the flags still outstanding, then sleep on the record's futex word
+    const int m = n - from;
+    rec->seq.fetch_add(1, std::memory_order_relaxed);  // odd: fields changing
+    std::atomic_thread_fence(std::memory_order_release);
+    for (int i = 0; i < m; ++i) {
+      rec->flags[i].store(flags[from + i], std::memory_order_relaxed);
+      rec->wants[i].store(wants[from + i], std::memory_order_relaxed);
     }
-    cv_.notify_one();
-    {
-      std::unique_lock<std::mutex> lk(pk.m);
-      pk.cv.wait_for(lk, slice, [&] { return pk.woken; });
+    rec->n.store(m, std::memory_order_relaxed);
+    rec->word.store(0, std::memory_order_relaxed);
+    rec->seq.fetch_add(1, std::memory_order_release);  // even: published
+    rec->active.store(1, std::memory_order_seq_cst);
+    if (sleeping_.load(std::memory_order_seq_cst) > 0) {  // a poller sleeps: new work for it
+      epoch_.fetch_add(1, std::memory_order_seq_cst);
+      futex_wake(&epoch_, INT32_MAX);
     }
-    {
-      // still listed: take it out (the poller wakes only listed waiters, under mu_)
-      std::lock_guard<std::mutex> lk(mu_);
-      auto it = std::find(parked_.begin(), parked_.end(), &pk);
-      if (it != parked_.end()) parked_.erase(it);
+    const auto deadline = t0 + slice;
+    while (rec->word.load(std::memory_order_acquire) == 0 && !reached_all(flags, wants, n, from)) {
+      const auto now = std::chrono::steady_clock::now();
+      if (now >= deadline) break;
+      futex_wait(&rec->word, 0, std::chrono::duration_cast<std::chrono::nanoseconds>(deadline - now));
     }
-    if (!reached(flag, want)) return false;
+    rec->active.store(0, std::memory_order_release);
+    if (!reached_all(flags, wants, n, from)) return false;
     note(t0);
     return true;
   }
+  bool wait(const unsigned *flag, unsigned want, std::chrono::microseconds slice) {
+    return wait(&flag, &want, 1, slice);
+  }
 
  private:
-  struct Parked {
-    const unsigned *flag;
-    unsigned want;
-    std::mutex m;
-    std::condition_variable cv;
-    bool woken = false;
+  static constexpr int kMaxRecords = 4096;  // threads that have parked at least once
+
+  struct alignas(64) Record {
+    std::atomic<uint32_t> seq{0};   // sequence lock over n / flags / wants (odd while writing)
+    std::atomic<uint32_t> word{0};  // futex word: set to 1 by the poller that wakes the waiter
+    std::atomic<int> active{0};     // 1 while the waiter is parked
+    std::atomic<int> n{0};
+    std::atomic<const unsigned *> flags[kMaxFlags];
+    std::atomic<unsigned> wants[kMaxFlags];
   };
+
+  // this thread's record; a thread that exits returns it for reuse
+  Record *my_record() {
+    struct Owner {
+      int idx = -1;
+      ~Owner() {
+        if (idx >= 0) FlagWaits::get().free_record(idx);
+      }
+    };
+    static thread_local Owner own;
+    if (own.idx < 0) own.idx = alloc_record();
+    return own.idx < 0 ? nullptr : &records_[own.idx];
+  }
+  int alloc_record() {
+    std::lock_guard<std::mutex> lk(free_mu_);
+    if (!free_.empty()) {
+      const int i = free_.back();
+      free_.pop_back();
+      return i;
+    }
+    const int i = used_.load(std::memory_order_relaxed);
+    if (i >= kMaxRecords) return -1;
+    used_.store(i + 1, std::memory_order_release);
+    return i;
+  }
+  void free_record(int i) {
+    records_[i].active.store(0, std::memory_order_release);
+    std::lock_guard<std::mutex> lk(free_mu_);
+    free_.push_back(i);
+  }
+
+  static void futex_wait(std::atomic<uint32_t> *w, uint32_t v, std::chrono::nanoseconds t) {
+    struct timespec ts;
+    ts.tv_sec = static_cast<time_t>(t.count() / 1000000000);
+    ts.tv_nsec = static_cast<long>(t.count() % 1000000000);
+    syscall(SYS_futex, reinterpret_cast<uint32_t *>(w), FUTEX_WAIT_PRIVATE, v, &ts, nullptr, 0);
+  }
+  static void futex_wake(std::atomic<uint32_t> *w, int n) {
+    syscall(SYS_futex, reinterpret_cast<uint32_t *>(w), FUTEX_WAKE_PRIVATE, n, nullptr, nullptr, 0);
+  }
 
   // moving average of completed waits (us), 1/8 weight per sample
   void note(std::chrono::steady_clock::time_point t0) {
@@ -1952,9 +2055,14 @@ class FlagWaits {
   static bool reached(const unsigned *flag, unsigned want) {
     return static_cast<int>(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - want) >= 0;
   }
+  // all of flags[from, n) reached; advances `from` past the ones that are
+  static bool reached_all(const unsigned *const *flags, const unsigned *wants, int n, int &from) {
+    while (from < n && reached(flags[from], wants[from])) ++from;
+    return from == n;
+  }
 
   FlagWaits() {
-    const char *n = getenv("LSEC_WAIT_SPINNERS"), *us = getenv("LSEC_WAIT_SPIN_US");
+    const char *n = getenv("LSEC_WAIT_SPINNERS"), *us = getenv("LSEC_WAIT_SPIN_US"), *np = getenv("LSEC_WAIT_POLLERS");
     // defaults from tools/gpu_wait_sweep.sh (profiles/r02_v22_wait_sweep.jsonl): a quarter of the
     // usable CPUs spin, for up to 30 us (an unloaded call completes in 14-20 us)
     spin_limit_ = n ? std::max(0, atoi(n)) : std::max(1, usable_cpus() / 4);
@@ -1962,33 +2070,51 @@ class FlagWaits {
     const char *w = getenv("LSEC_WAIT"), *ad = getenv("LSEC_WAIT_ADAPT");
     spin_only_ = w && strcmp(w, "spin") == 0;
     adapt_ = !ad || atoi(ad) != 0;
-    if (!spin_only_) std::thread([this] { poll(); }).detach();
+    // pollers: one per 8 usable CPUs, at most 4 (LSEC_WAIT_POLLERS)
+    npollers_ = np ? std::max(1, std::min(16, atoi(np))) : std::max(1, std::min(4, usable_cpus() / 8));
+    if (!spin_only_)
+      for (int p = 0; p < npollers_; ++p) std::thread([this, p] { poll(p); }).detach();
   }
 
-  void poll() {
-    std::unique_lock<std::mutex> lk(mu_);
+  // poller p scans records p, p + npollers, ...: wakes every parked waiter whose flags have all
+  // come; sleeps on epoch_ while none of its records is parked
+  void poll(int p) {
+    const unsigned *f[kMaxFlags];
+    unsigned wv[kMaxFlags];
     for (;;) {
-      cv_.wait(lk, [&] { return !parked_.empty(); });
-      for (size_t i = 0; i < parked_.size();) {
-        Parked *p = parked_[i];
-        if (reached(p->flag, p->want)) {
-          {
-            std::lock_guard<std::mutex> g(p->m);
-            p->woken = true;
-          }
-          p->cv.notify_one();  // under mu_: the waiter cannot unlist and free it meanwhile
-          parked_[i] = parked_.back();
-          parked_.pop_back();
-        } else {
-          ++i;
+      bool any = false;
+      const int hi = used_.load(std::memory_order_acquire);
+      for (int i = p; i < hi; i += npollers_) {
+        Record &r = records_[i];
+        if (!r.active.load(std::memory_order_acquire)) continue;
+        any = true;
+        const uint32_t s1 = r.seq.load(std::memory_order_acquire);
+        if (s1 & 1u) continue;
+        const int m = r.n.load(std::memory_order_relaxed);
+        if (m < 1 || m > kMaxFlags) continue;
+        for (int j = 0; j < m; ++j) {
+          f[j] = r.flags[j].load(std::memory_order_relaxed);
+          wv[j] = r.wants[j].load(std::memory_order_relaxed);
         }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if (r.seq.load(std::memory_order_relaxed) != s1) continue;  // rewritten meanwhile
+        int from = 0;
+        if (!reached_all(f, wv, m, from)) continue;
+        if (r.word.exchange(1, std::memory_order_acq_rel) == 0) futex_wake(&r.word, 1);
       }
-      if (!parked_.empty()) {  // flags are written by the GPU: poll, a few us apart
-        lk.unlock();
+      if (any) {  // flags are written by the GPU: poll, a few us apart
         for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
         std::this_thread::yield();
-        lk.lock();
+        continue;
       }
+      // nothing parked here: sleep until a waiter parks (it bumps epoch_ when it sees a sleeper)
+      const uint32_t e = epoch_.load(std::memory_order_seq_cst);
+      sleeping_.fetch_add(1, std::memory_order_seq_cst);
+      bool now_any = false;
+      const int hi2 = used_.load(std::memory_order_acquire);
+      for (int i = p; i < hi2 && !now_any; i += npollers_) now_any = records_[i].active.load(std::memory_order_seq_cst) != 0;
+      if (!now_any) futex_wait(&epoch_, e, std::chrono::milliseconds(10));
+      sleeping_.fetch_sub(1, std::memory_order_seq_cst);
     }
   }
 
@@ -1996,11 +2122,15 @@ class FlagWaits {
   std::chrono::microseconds spin_{100};  // how long one spins before parking (LSEC_WAIT_SPIN_US)
   bool spin_only_ = false;
   bool adapt_ = true;  // no spinning while recent waits are long (LSEC_WAIT_ADAPT=0: always)
+  int npollers_ = 1;
   std::atomic<int> spinners_{0};
   std::atomic<long> recent_us_{0};
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::vector<Parked *> parked_;
+  std::atomic<uint32_t> epoch_{0};
+  std::atomic<int> sleeping_{0};
+  std::atomic<int> used_{0};
+  Record records_[kMaxRecords];
+  std::mutex free_mu_;
+  std::vector<int> free_;
 };
 
 // Waits until flag reaches v (wrapping u32 sequence) through FlagWaits.  Bounded: after 2 s
@@ -2017,6 +2147,26 @@ bool wait_flag(const unsigned *flag, unsigned v, hipStream_t st, int *rc) {
   }
   return true;
 }
+
+// Routes taken by zero-copy calls, printed at exit with LSEC_STATS=1: served by the stripe
+// server, refused by it (no free slots: claim failed, or not servable), then run as their own
+// launch (kernel over the caller's page-locked chunks, or over this thread's slot)
+struct ZcStats {
+  std::atomic<unsigned long long> server{0}, no_slots{0}, not_servable{0}, launch_direct{0}, launch_slot{0};
+  static ZcStats &get() {
+    static ZcStats *s = [] {
+      ZcStats *p = new ZcStats();  // leaked: read by the atexit printer
+      if (getenv("LSEC_STATS")) atexit([] {
+        ZcStats &z = get();
+        fprintf(stderr, "[lsec stats] zero-copy calls: server %llu, server out of slots %llu, not servable %llu, "
+                "own launch (caller page-locked) %llu, own launch (slot) %llu\n", z.server.load(), z.no_slots.load(),
+                z.not_servable.load(), z.launch_direct.load(), z.launch_slot.load());
+      });
+      return p;
+    }();
+    return *s;
+  }
+};
 
 // ---------------------------------------------------------------- stripe server (host side)
 // Per-stripe calls up to kSlotBytes per part are served by the persistent stripe server
@@ -2046,15 +2196,19 @@ class StripeServer {
   int run(PlanExt *e, char **ptrs, long long C, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
           const void *image, int kind, const CallerPinned *cp) {
     const size_t nin = in_ids.size(), nout = out_ids.size(), nio = nin + nout;
-    if (nin < 1 || nout < 1 || nin > lsec::kSrvMaxK || nout > lsec::kSrvMaxR) return 1;
-    if (kind != KBYTEWISE && kind != KBITSLICED) return 1;
+    const auto refuse = [] {
+      ZcStats::get().not_servable.fetch_add(1, std::memory_order_relaxed);
+      return 1;
+    };
+    if (nin < 1 || nout < 1 || nin > lsec::kSrvMaxK || nout > lsec::kSrvMaxR) return refuse();
+    if (kind != KBYTEWISE && kind != KBITSLICED) return refuse();
     const lio_erasure_plan_t *p = &e->pub;
     const bool direct = cp && cp->by_kernel;
     // parts: column blocks of about 4 KiB per shard (one 256-lane x 16 B pass), whole
     // super-packets for the bit-sliced layout, at most kMaxParts of them
     const long long unit = kind == KBITSLICED ? 8LL * p->packet_size : 16;
     const long long max_len = direct ? C : static_cast<long long>(kSlotBytes / nio) / unit * unit;
-    if (max_len < std::min<long long>(unit, C)) return 1;
+    if (max_len < std::min<long long>(unit, C)) return refuse();
     static const long long target = [] {  // column bytes per part (LSEC_SRV_PART_KB, A/B runs)
       const char *v = getenv("LSEC_SRV_PART_KB");
       return v ? std::max(1LL, atoll(v)) << 10 : 4096LL;
@@ -2062,12 +2216,31 @@ class StripeServer {
     long long len = std::min(std::max<long long>(unit, target / unit * unit), max_len);
     if ((C + len - 1) / len > kMaxParts) {
       len = ((C + kMaxParts - 1) / kMaxParts + unit - 1) / unit * unit;
-      if (len > max_len) return 1;
+      if (len > max_len) return refuse();
     }
     if (len > C) len = C;
-    const int nparts = static_cast<int>((C + len - 1) / len);
+    int nparts = static_cast<int>((C + len - 1) / len);
     int slot[kMaxParts];
-    if (!claim(nparts, slot)) return 1;
+    if (!claim(nparts, slot)) {
+      // under load: fewer, larger parts (as many columns as a slot holds), then a short wait for
+      // slots to come free -- the other route, a launch of this call's own, costs the host far
+      // more CPU per call than a wait (profiles/r02_v28_zc_routes.txt)
+      bool got = false;
+      if (len < std::min(max_len, C)) {
+        len = std::min(max_len, C);
+        nparts = static_cast<int>((C + len - 1) / len);
+        got = claim(nparts, slot);
+      }
+      const auto t0 = std::chrono::steady_clock::now();
+      while (!got && std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(50)) {
+        std::this_thread::yield();
+        got = claim(nparts, slot);
+      }
+      if (!got) {
+        ZcStats::get().no_slots.fetch_add(1, std::memory_order_relaxed);
+        return 1;
+      }
+    }
     if (init_once()) {
       release(nparts, slot);
       return -1;
@@ -2103,20 +2276,20 @@ class StripeServer {
     int rc = ensure_running(false);
     const auto t0 = std::chrono::steady_clock::now();
     auto last_check = t0;
-    for (int q = 0; q < nparts && rc == 0; ++q) {
-      const uint32_t *flag = &sh_->done[slot[q]][0];
-      // spin or park (FlagWaits), checking every 100 us that the server has not retired meanwhile
-      while (!FlagWaits::get().wait(flag, want[q], std::chrono::microseconds(100))) {
-        const auto now = std::chrono::steady_clock::now();
-        if (now - last_check > std::chrono::microseconds(100)) {
-          last_check = now;
-          if ((rc = ensure_running(true))) break;
-        }
-        if (now - t0 > std::chrono::seconds(5)) {
-          rc = fail("stripe server: no answer for 5 s");
-          broken_ = true;
-          break;
-        }
+    const unsigned *flags[kMaxParts];
+    for (int q = 0; q < nparts; ++q) flags[q] = &sh_->done[slot[q]][0];
+    // spin or park (FlagWaits) until every part is done, checking every 100 us that the server
+    // has not retired meanwhile
+    while (rc == 0 && !FlagWaits::get().wait(flags, want, nparts, std::chrono::microseconds(100))) {
+      const auto now = std::chrono::steady_clock::now();
+      if (now - last_check > std::chrono::microseconds(100)) {
+        last_check = now;
+        if ((rc = ensure_running(true))) break;
+      }
+      if (now - t0 > std::chrono::seconds(5)) {
+        rc = fail("stripe server: no answer for 5 s");
+        broken_ = true;
+        break;
       }
     }
     static const bool trace = getenv("LSEC_TRACE") != nullptr;
@@ -2174,7 +2347,9 @@ class StripeServer {
     for (int k = 0; k < lsec::kSrvSlots && got < n; ++k) {
       const int s = static_cast<int>((base + k) % lsec::kSrvSlots);
       uint8_t z = 0;
-      if (busy_[s].compare_exchange_strong(z, 1)) slot[got++] = s;
+      // look before the locked exchange: under load most slots are busy, and a failed
+      // exchange on every one of them from every thread kept the flag lines bouncing
+      if (busy_[s].load(std::memory_order_relaxed) == 0 && busy_[s].compare_exchange_strong(z, 1)) slot[got++] = s;
     }
     if (got < n) {
       release(got, slot);
@@ -2292,13 +2467,17 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
   CallerPinned cp = caller_pinned(ptrs, nstripes, km, in_ids, out_ids, C, aligned);
   if (nstripes == 1 && server_enabled()) {
     const int rc = StripeServer::for_device(dev)->run(e, ptrs, C, in_ids, out_ids, image, kind, &cp);
-    if (rc != 1) return rc;
+    if (rc != 1) {
+      if (rc == 0) ZcStats::get().server.fetch_add(1, std::memory_order_relaxed);
+      return rc;
+    }
   }
   std::vector<int64_t> stride;
   if (cp.by_kernel && regular_refs(cp.dev, nstripes, nio, stride)) {
     // caller page-locked chunks: read and written in place over PCIe
     for (size_t j = 0; j < nin; ++j) in[j] = {cp.dev[j], stride[j]};
     for (size_t r = 0; r < nout; ++r) out[r] = {cp.dev[nin + r], stride[nin + r]};
+    ZcStats::get().launch_direct.fetch_add(1, std::memory_order_relaxed);
     if (enqueue_apply(kind, image, static_cast<int>(nin), static_cast<int>(nout), in, out, nstripes, C, p->packet_size, st, p->w))
       return -1;
     return zc_complete(*slot, st);
@@ -2316,6 +2495,7 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
     slot->d = reinterpret_cast<uint64_t>(d);
     slot->cap = cap;
   }
+  ZcStats::get().launch_slot.fetch_add(1, std::memory_order_relaxed);
   // slot layout: inputs [s][nin][C], then outputs [s][nout][C]
   const size_t in_bytes = static_cast<size_t>(nstripes) * nin * C;
   for (int s = 0; s < nstripes; ++s)

@@ -13,7 +13,7 @@ namespace lsec {
 #define LSEC_SRV_WG 32
 #endif
 constexpr int kSrvWG = LSEC_SRV_WG;  // server workgroups (one per CU they land on)
-constexpr int kSrvSlotsPerWG = 15;  // post line word 15 is the stop word
+constexpr int kSrvSlotsPerWG = 31;  // post words 0-30 (two 64-byte lines); word 31 is the stop word
 constexpr int kSrvSlots = kSrvWG * kSrvSlotsPerWG;
 constexpr int kSrvMaxK = 32;        // inputs of one request the server takes
 constexpr int kSrvMaxR = 8;         // outputs of one request the server takes
@@ -37,7 +37,7 @@ struct SrvDesc {
 
 // page-locked coherent host memory shared by the host threads and the server
 struct SrvShared {
-  uint32_t post[kSrvWG][16];
+  uint32_t post[kSrvWG][32];
   uint32_t done[kSrvSlots][16];  // done[s][0]; one 64-byte line per slot
   SrvDesc desc[kSrvSlots];
 };

@@ -5,12 +5,12 @@
 // live in page-locked host memory (or the caller's own page-locked buffers), and the serving
 // workgroup reads and writes them over PCIe -- no DMA, no launch per call.
 //
-// Protocol (one 64-byte line per workgroup, so one PCIe read polls all its slots):
+// Protocol (two 64-byte lines per workgroup, so one wave-wide PCIe read polls all its slots):
 //   host   writes desc[s], then post[g][i] = n  (n: the slot's next sequence number)
 //   server sees post != served, acquires, copies desc (and the coefficient cells) into LDS,
 //          computes, releases at system scope, writes done[s] = n
 //   host   spins on done[s] == n, copies the outputs out, frees the slot
-// post[g][15] is the stop word.  The kernel exits when every workgroup has been idle for
+// post[g][31] is the stop word.  The kernel exits when every workgroup has been idle for
 // idle_ticks (a collective vote, below) or when the stop word is set -- every wave reaches
 // one of them -- and the host relaunches it on demand.  It runs on its own high-priority stream: such a stream has a hardware queue of its
 // own, so the parked kernel never holds up other streams' packets (tools/probes/queue_probe.hip,
@@ -147,7 +147,7 @@ __device__ void srv_serve(const SrvDesc &d, const CoefCell *cl) {
 __global__ __launch_bounds__(kBlock) void k_stripe_server(SrvArgs a) {
   __shared__ SrvDesc d;
   __shared__ CoefCell cl[kSrvMaxR * kSrvMaxK];
-  __shared__ uint32_t served[16];
+  __shared__ uint32_t served[32];
   __shared__ int pick, quit, last_pick, voted;
   __shared__ uint32_t pick_val;
   __shared__ uint64_t idle_since;
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(kBlock) void k_stripe_server(SrvArgs a) {
   for (;;) {
     if (threadIdx.x < 64) {  // wave 0 polls this workgroup's line
       const int lane = threadIdx.x;
-      const uint32_t v = lane < 16 ? sys_load(&sh->post[g][lane]) : 0u;
+      const uint32_t v = lane < 32 ? sys_load(&sh->post[g][lane]) : 0u;
       const bool ready = lane < kSrvSlotsPerWG && v != served[lane];
       const uint64_t m = __ballot(ready);
       const uint32_t stop = __shfl(v, kSrvSlotsPerWG);
