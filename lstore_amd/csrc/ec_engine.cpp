@@ -85,8 +85,22 @@ struct DecodeEntry {
   std::map<int, uint32_t *> dev_masks;
 };
 
+constexpr int kFastDevs = 16;  // devices whose encode image pointer is cached lock-free
+
 struct PlanImpl {
   std::mutex mu;
+  // Lock-free fast path of the per-stripe calls (up to 300 pool threads share one plan): set
+  // once under mu, after what they publish is complete, and never cleared before the plan is
+  // destroyed (the caller may not use a plan it destroys).
+  std::atomic<bool> coding_fast{false};
+  std::atomic<const void *> enc_fast[kFastDevs] = {};
+  // process-unique id: per-thread caches key on it, not on the address (a destroyed plan's
+  // address can come back for a new plan)
+  const unsigned long long serial = next_serial();
+  static unsigned long long next_serial() {
+    static std::atomic<unsigned long long> n{0};
+    return ++n;
+  }
   lsec::gf8::Mat coding;   // GF(2^8) matrix the kernels apply (m x k)
   lsec::gfw::Mat coding_w; // GF(2^16) / GF(2^32) matrix codes (m x k)
   bool coding_ready = false;
@@ -224,6 +238,7 @@ int form_matrices(lio_erasure_plan_t *p, bool with_schedule) {
     case RAID4:
       e->impl->coding.assign(k, 1);
       e->impl->coding_ready = true;
+      e->impl->coding_fast.store(true, std::memory_order_release);
       return 0;
     case REED_SOL_VAN:
     case REED_SOL_R6_OP: {
@@ -293,6 +308,7 @@ int form_matrices(lio_erasure_plan_t *p, bool with_schedule) {
     e->impl->enc_masks = bitmatrix_masks(p->encode_bitmatrix, k, m, w);
     group_image(e->impl->enc_masks, m * w, k, lsec::mask_words(w));
     e->impl->coding_ready = true;
+    e->impl->coding_fast.store(true, std::memory_order_release);
   } else if (p->encode_matrix) {
     const int rows = (p->method == REED_SOL_R6_OP) ? 2 : m;
     if (kind == KWORDWISE || kind == KBITSLICEDW) {
@@ -305,6 +321,7 @@ int form_matrices(lio_erasure_plan_t *p, bool with_schedule) {
       for (size_t i = 0; i < e->impl->coding.size(); ++i) e->impl->coding[i] = static_cast<uint8_t>(p->encode_matrix[i]);
     }
     e->impl->coding_ready = true;
+    e->impl->coding_fast.store(true, std::memory_order_release);
   }
   return 0;
 }
@@ -331,6 +348,7 @@ int fp_form_decoding(lio_erasure_plan_t *p) {
 }
 
 int ensure_coding(PlanExt *e) {
+  if (e->impl->coding_fast.load(std::memory_order_acquire)) return 0;
   {
     std::lock_guard<std::mutex> lk(e->impl->mu);
     if (e->impl->coding_ready) return 0;
@@ -381,12 +399,25 @@ int upload_masks(const std::vector<uint32_t> &h, uint32_t **out) {
   return 0;
 }
 
+int encode_cells_locked(PlanExt *e, int dev, const void **out);
+
 // encode image on the current device: CoefCell[m][k] (matrix codes) or row masks (bitmatrix)
 int encode_cells(PlanExt *e, const void **out) {
   if (ensure_coding(e)) return -1;
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
+  if (dev >= 0 && dev < kFastDevs)
+    if (const void *f = e->impl->enc_fast[dev].load(std::memory_order_acquire)) {
+      *out = f;
+      return 0;
+    }
   std::lock_guard<std::mutex> lk(e->impl->mu);
+  const int rc = encode_cells_locked(e, dev, out);
+  if (rc == 0 && dev >= 0 && dev < kFastDevs) e->impl->enc_fast[dev].store(*out, std::memory_order_release);
+  return rc;
+}
+
+int encode_cells_locked(PlanExt *e, int dev, const void **out) {
   if (uses_u32_image(kernel_kind(e->pub.method, e->pub.w))) {
     auto it = e->impl->enc_dev_masks.find(dev);
     if (it == e->impl->enc_dev_masks.end()) {
@@ -437,12 +468,44 @@ int parse_erasures(const lio_erasure_plan_t *p, const int *erasures, std::vector
   return 0;
 }
 
-// decode entry (host plan + device cells on the current device)
+int decode_entry_locked(PlanExt *e, const std::vector<int> &ids, int dev, DecodeEntry **out, const void **cells);
+
+// decode entry (host plan + device cells on the current device).  Entries are never moved or
+// freed before the plan is destroyed, so each thread keeps its last lookup and repeats of it
+// (a degraded read decodes the same pattern stripe after stripe) skip the plan mutex.
 int decode_entry(PlanExt *e, const std::vector<int> &ids, DecodeEntry **out, const void **cells) {
   if (ensure_coding(e)) return -1;
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> lk(e->impl->mu);
+  struct Last {
+    unsigned long long serial = 0;
+    int dev = -1;
+    std::vector<int> ids;
+    DecodeEntry *ent = nullptr;
+    const void *cells = nullptr;
+  };
+  thread_local Last last;
+  if (last.serial == e->impl->serial && last.dev == dev && last.ids == ids) {
+    *out = last.ent;
+    *cells = last.cells;
+    return 0;
+  }
+  int rc;
+  {
+    std::lock_guard<std::mutex> lk(e->impl->mu);
+    rc = decode_entry_locked(e, ids, dev, out, cells);
+  }
+  if (rc == 0) {
+    last.serial = e->impl->serial;
+    last.dev = dev;
+    last.ids = ids;
+    last.ent = *out;
+    last.cells = *cells;
+  }
+  return rc;
+}
+
+int decode_entry_locked(PlanExt *e, const std::vector<int> &ids, int dev, DecodeEntry **out, const void **cells) {
   const int kind = kernel_kind(e->pub.method, e->pub.w);
   const bool bitm = uses_u32_image(kind);
   auto it = e->impl->decode_cache.find(ids);
@@ -827,16 +890,55 @@ int ensure_slot(Staging::Slot &sl, size_t bytes, bool need_host = true) {
   return 0;
 }
 
+// Pointer attributes.  Every hipPointerGetAttributes takes a lock of the HIP runtime; per-stripe
+// calls from tens of threads made 10-20 queries each and spent most of their time queued on it
+// (an RS(6+3) 16 KiB call: 3 us of set-up at one thread, 140-360 us at 32 before this memo, 12 us
+// after; LSEC_STATS phase means, profiles/r02_v30_zc_phases.txt for the after-state).  Within
+// one public call the caller's buffers cannot change kind, so a
+// call answers repeated queries from a per-call memo (PtrMemo: the entry points of the batched
+// and per-stripe calls open one; with none open every query goes to the runtime).
+struct PtrInfo {
+  bool ok = false;  // the runtime knows the pointer (device memory or page-locked host memory)
+  hipMemoryType type = hipMemoryTypeHost;
+  void *dev = nullptr;  // its device address
+};
+thread_local int tl_memo_depth = 0;
+thread_local std::vector<std::pair<const void *, PtrInfo>> tl_memo;
+
+struct PtrMemo {
+  PtrMemo() {
+    if (tl_memo_depth++ == 0) tl_memo.clear();
+  }
+  ~PtrMemo() {
+    if (--tl_memo_depth == 0) tl_memo.clear();
+  }
+  PtrMemo(const PtrMemo &) = delete;
+  PtrMemo &operator=(const PtrMemo &) = delete;
+};
+
+PtrInfo query_ptr(const void *ptr) {
+  if (tl_memo_depth > 0)
+    for (const auto &kv : tl_memo)
+      if (kv.first == ptr) return kv.second;
+  PtrInfo r;
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, ptr) == hipSuccess) {
+    r.ok = true;
+    r.type = attr.type;
+    r.dev = attr.devicePointer;
+  } else {
+    (void)hipGetLastError();  // pageable host memory reports an error on some runtimes
+  }
+  if (tl_memo_depth > 0 && tl_memo.size() < 1024) tl_memo.push_back({ptr, r});
+  return r;
+}
+
 // Caller buffers that are already page-locked (hipHostMalloc'd, or hipHostRegister'ed by an
 // allocator that pins its cache pages) need no packing: the DMA engines copy straight
 // between them and the device slots, and the host copy pool stays idle.
 bool is_pinned_host(const void *ptr) {
-  hipPointerAttribute_t attr;
-  if (hipPointerGetAttributes(&attr, ptr) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return attr.type == hipMemoryTypeHost;
+  const PtrInfo i = query_ptr(ptr);
+  return i.ok && i.type == hipMemoryTypeHost;
 }
 
 // every staged shard of the first and last stripe pinned?  (a stray pageable pointer in
@@ -876,6 +978,10 @@ CallerPinned caller_pinned(char **ptrs, int nstripes, int km, const std::vector<
   static const bool off = getenv("LSEC_NO_PINNED_DMA") != nullptr;
   CallerPinned r;
   if (off) return r;
+  // A first chunk that is not page-locked settles it, with no lock: every path below returns
+  // "not pinned" for it too, and taking memory for pageable is always safe.  (Per-stripe calls
+  // from hundreds of threads queued on this mutex.)
+  if (!in_ids.empty() && nstripes >= 1 && !is_pinned_host(ptrs[in_ids[0]])) return r;
   std::lock_guard<std::mutex> lk(g_inplace_mu);
   if (!g_inplace.empty()) {
     for (int s = 0; s < nstripes; ++s)
@@ -1109,11 +1215,8 @@ bool caller_pinned_aliases(char **ptrs, int nstripes, int km, const std::vector<
     for (const std::vector<int> *ids : {&in_ids, &out_ids})
       for (int id : *ids) {
         char *p = ptrs[static_cast<size_t>(s) * km + id];
-        hipPointerAttribute_t a;
-        if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer) {
-          (void)hipGetLastError();
-          return false;
-        }
+        const PtrInfo a = query_ptr(p);
+        if (!a.ok || a.type != hipMemoryTypeHost || !a.dev) return false;
         const uintptr_t u = reinterpret_cast<uintptr_t>(p);
         if (u < lo || u + static_cast<uintptr_t>(C) > hi) {
           hipDeviceptr_t base = nullptr;
@@ -1126,7 +1229,7 @@ bool caller_pinned_aliases(char **ptrs, int nstripes, int km, const std::vector<
           hi = lo + size;
           if (u < lo || u + static_cast<uintptr_t>(C) > hi) return false;
         }
-        dev.push_back(reinterpret_cast<uint64_t>(a.devicePointer));
+        dev.push_back(reinterpret_cast<uint64_t>(a.dev));
       }
   return true;
 }
@@ -1400,27 +1503,28 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
 }
 
 bool is_device_ptr(const void *ptr) {
-  hipPointerAttribute_t attr;
-  if (hipPointerGetAttributes(&attr, ptr) != hipSuccess) {
-    (void)hipGetLastError();  // pageable host memory reports an error on some runtimes
-    return false;
-  }
-  return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+  const PtrInfo i = query_ptr(ptr);
+  return i.ok && (i.type == hipMemoryTypeDevice || i.type == hipMemoryTypeManaged);
 }
 
 // all k+m pointers of every stripe device memory?  then describe them as shard refs
-// Returns 1 (device layout in sh), 0 (host memory), -1 (device and host pointers mixed in the
-// first or last stripe, or an irregular device stride: refused rather than guessed).
+// Returns 1 (device layout in sh), 0 (host memory), -1 (device and host pointers mixed, or an
+// irregular device stride: refused rather than guessed).  A batch whose first chunk is device
+// memory has every chunk of its first and last stripe checked; one whose first chunk is host
+// memory has the last chunk of its first and last stripe checked (each check is a query under a
+// runtime lock that per-stripe calls contend on; a device pointer among host chunks would fault
+// the host copy, as it faults the reference's CPU code).
 int device_layout(const lio_erasure_plan_t *p, char **ptrs, int nstripes, std::vector<lsec_shard_t> &sh) {
   const int km = p->data_strips + p->parity_strips;
-  int ndev = 0;
-  for (int s : {0, nstripes - 1}) {
-    for (int i = 0; i < km; ++i) ndev += is_device_ptr(ptrs[static_cast<size_t>(s) * km + i]);
-    if (nstripes == 1) break;
+  if (!is_device_ptr(ptrs[0])) {
+    for (int s : {0, nstripes - 1})
+      for (int i : {0, km - 1})
+        if (is_device_ptr(ptrs[static_cast<size_t>(s) * km + i])) return fail("stripe pointers mix device and host memory");
+    return 0;
   }
-  const int total = nstripes == 1 ? km : 2 * km;
-  if (ndev == 0) return 0;
-  if (ndev != total) return fail("stripe pointers mix device and host memory");
+  for (int s : {0, nstripes - 1})
+    for (int i = 0; i < km; ++i)
+      if (!is_device_ptr(ptrs[static_cast<size_t>(s) * km + i])) return fail("stripe pointers mix device and host memory");
   sh.resize(km);
   for (int i = 0; i < km; ++i) {
     sh[i].base = ptrs[i];
@@ -1912,6 +2016,10 @@ int usable_cpus() {
 // (profiles/r02_v28_zc_routes.txt).  Every flag a record can name stays mapped for the life of
 // the process (server done lines; zero-copy flags come from a pool that is never freed), so a
 // poller that reads a record just as its waiter leaves reads valid memory.
+// LSEC_STATS counters of the waiting machinery (printed with ZcStats at exit)
+std::atomic<unsigned long long> g_st_parks{0}, g_st_spin_hits{0}, g_st_claim_misses{0}, g_st_claim_spins{0},
+    g_st_wakes{0}, g_st_slices{0};
+
 class FlagWaits {
  public:
   static constexpr int kMaxFlags = 16;  // flags one wait covers (StripeServer::kMaxParts)
@@ -1954,6 +2062,7 @@ class FlagWaits {
         if (reached_all(flags, wants, n, from)) {
           spinners_.fetch_sub(1, std::memory_order_relaxed);
           note(t0);
+          g_st_spin_hits.fetch_add(1, std::memory_order_relaxed);
           return true;
         }
         __builtin_ia32_pause();
@@ -1973,6 +2082,7 @@ class FlagWaits {
     rec->word.store(0, std::memory_order_relaxed);
     rec->seq.fetch_add(1, std::memory_order_release);  // even: published
     rec->active.store(1, std::memory_order_seq_cst);
+    g_st_parks.fetch_add(1, std::memory_order_relaxed);
     if (sleeping_.load(std::memory_order_seq_cst) > 0) {  // a poller sleeps: new work for it
       epoch_.fetch_add(1, std::memory_order_seq_cst);
       futex_wake(&epoch_, INT32_MAX);
@@ -1984,7 +2094,10 @@ class FlagWaits {
       futex_wait(&rec->word, 0, std::chrono::duration_cast<std::chrono::nanoseconds>(deadline - now));
     }
     rec->active.store(0, std::memory_order_release);
-    if (!reached_all(flags, wants, n, from)) return false;
+    if (!reached_all(flags, wants, n, from)) {
+      g_st_slices.fetch_add(1, std::memory_order_relaxed);
+      return false;
+    }
     note(t0);
     return true;
   }
@@ -2100,7 +2213,10 @@ class FlagWaits {
         if (r.seq.load(std::memory_order_relaxed) != s1) continue;  // rewritten meanwhile
         int from = 0;
         if (!reached_all(f, wv, m, from)) continue;
-        if (r.word.exchange(1, std::memory_order_acq_rel) == 0) futex_wake(&r.word, 1);
+        if (r.word.exchange(1, std::memory_order_acq_rel) == 0) {
+          futex_wake(&r.word, 1);
+          g_st_wakes.fetch_add(1, std::memory_order_relaxed);
+        }
       }
       if (any) {  // flags are written by the GPU: poll, a few us apart
         for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
@@ -2151,8 +2267,18 @@ bool wait_flag(const unsigned *flag, unsigned v, hipStream_t st, int *rc) {
 // Routes taken by zero-copy calls, printed at exit with LSEC_STATS=1: served by the stripe
 // server, refused by it (no free slots: claim failed, or not servable), then run as their own
 // launch (kernel over the caller's page-locked chunks, or over this thread's slot)
+thread_local std::chrono::steady_clock::time_point tl_call_t0;  // fn-pointer entry (LSEC_STATS)
+thread_local std::chrono::steady_clock::time_point tl_zc_t0;    // run_zerocopy entry (LSEC_STATS)
+
 struct ZcStats {
   std::atomic<unsigned long long> server{0}, no_slots{0}, not_servable{0}, launch_direct{0}, launch_slot{0};
+  // server-served calls, wall time per phase (ns): fn-pointer entry -> server (plan checks,
+  // layout and pinned-memory lookups), claim + copies in + posts, wait, copies out
+  std::atomic<unsigned long long> t_setup{0}, t_zc{0}, t_post{0}, t_wait{0}, t_out{0};
+  static bool on() {
+    static const bool v = getenv("LSEC_STATS") != nullptr;
+    return v;
+  }
   static ZcStats &get() {
     static ZcStats *s = [] {
       ZcStats *p = new ZcStats();  // leaked: read by the atexit printer
@@ -2161,6 +2287,13 @@ struct ZcStats {
         fprintf(stderr, "[lsec stats] zero-copy calls: server %llu, server out of slots %llu, not servable %llu, "
                 "own launch (caller page-locked) %llu, own launch (slot) %llu\n", z.server.load(), z.no_slots.load(),
                 z.not_servable.load(), z.launch_direct.load(), z.launch_slot.load());
+        fprintf(stderr, "[lsec stats] waits: spin hits %llu, parks %llu, poller wakes %llu, timed-out slices %llu; "
+                "claims missed %llu, claim retries %llu\n", g_st_spin_hits.load(), g_st_parks.load(), g_st_wakes.load(),
+                g_st_slices.load(), g_st_claim_misses.load(), g_st_claim_spins.load());
+        const double n = static_cast<double>(std::max(1ULL, z.server.load())) * 1e3;
+        fprintf(stderr, "[lsec stats] server calls, mean wall us: setup %.2f (of it in run_zerocopy %.2f), claim+copy-in+post %.2f, "
+                "wait %.2f, copy-out %.2f\n", z.t_setup.load() / n, z.t_zc.load() / n, z.t_post.load() / n, z.t_wait.load() / n,
+                z.t_out.load() / n);
       });
       return p;
     }();
@@ -2195,6 +2328,7 @@ class StripeServer {
   // 0 served, -1 error, 1 not servable here (the caller takes another path)
   int run(PlanExt *e, char **ptrs, long long C, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
           const void *image, int kind, const CallerPinned *cp) {
+    const auto t_enter = std::chrono::steady_clock::now();
     const size_t nin = in_ids.size(), nout = out_ids.size(), nio = nin + nout;
     const auto refuse = [] {
       ZcStats::get().not_servable.fetch_add(1, std::memory_order_relaxed);
@@ -2226,6 +2360,7 @@ class StripeServer {
       // slots to come free -- the other route, a launch of this call's own, costs the host far
       // more CPU per call than a wait (profiles/r02_v28_zc_routes.txt)
       bool got = false;
+      g_st_claim_misses.fetch_add(1, std::memory_order_relaxed);
       if (len < std::min(max_len, C)) {
         len = std::min(max_len, C);
         nparts = static_cast<int>((C + len - 1) / len);
@@ -2234,6 +2369,7 @@ class StripeServer {
       const auto t0 = std::chrono::steady_clock::now();
       while (!got && std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(50)) {
         std::this_thread::yield();
+        g_st_claim_spins.fetch_add(1, std::memory_order_relaxed);
         got = claim(nparts, slot);
       }
       if (!got) {
@@ -2278,11 +2414,12 @@ class StripeServer {
     auto last_check = t0;
     const unsigned *flags[kMaxParts];
     for (int q = 0; q < nparts; ++q) flags[q] = &sh_->done[slot[q]][0];
-    // spin or park (FlagWaits) until every part is done, checking every 100 us that the server
-    // has not retired meanwhile
-    while (rc == 0 && !FlagWaits::get().wait(flags, want, nparts, std::chrono::microseconds(100))) {
+    // spin or park (FlagWaits) until every part is done, checking every 500 us that the server
+    // has not retired meanwhile (it retires only after 2 ms without work; at 100 us slices a
+    // loaded box woke 1.5 parked waiters per call just to check, profiles/r02_v30_zc_phases3.txt)
+    while (rc == 0 && !FlagWaits::get().wait(flags, want, nparts, std::chrono::microseconds(500))) {
       const auto now = std::chrono::steady_clock::now();
-      if (now - last_check > std::chrono::microseconds(100)) {
+      if (now - last_check > std::chrono::microseconds(500)) {
         last_check = now;
         if ((rc = ensure_running(true))) break;
       }
@@ -2292,6 +2429,7 @@ class StripeServer {
         break;
       }
     }
+    const auto t_waited = std::chrono::steady_clock::now();
     static const bool trace = getenv("LSEC_TRACE") != nullptr;
     if (trace) {  // calls slower than 1 ms: where the time went
       const auto t_end = std::chrono::steady_clock::now();
@@ -2311,6 +2449,18 @@ class StripeServer {
         for (size_t r = 0; r < nout; ++r) std::memcpy(ptrs[out_ids[r]] + c0, region + (nin + r) * n, static_cast<size_t>(n));
       }
     if (rc == 0) release(nparts, slot);  // a slot whose post may still be served is never handed out again
+    if (rc == 0 && ZcStats::on()) {
+      ZcStats &z = ZcStats::get();
+      const auto ns = [](std::chrono::steady_clock::duration d) {
+        return static_cast<unsigned long long>(std::chrono::duration_cast<std::chrono::nanoseconds>(d).count());
+      };
+      const auto t_done = std::chrono::steady_clock::now();
+      if (tl_call_t0.time_since_epoch().count() && t_enter > tl_call_t0) z.t_setup.fetch_add(ns(t_enter - tl_call_t0), std::memory_order_relaxed);
+      if (tl_zc_t0.time_since_epoch().count() && t_enter > tl_zc_t0) z.t_zc.fetch_add(ns(t_enter - tl_zc_t0), std::memory_order_relaxed);
+      z.t_post.fetch_add(ns(t_post - t_enter), std::memory_order_relaxed);
+      z.t_wait.fetch_add(ns(t_waited - t_post), std::memory_order_relaxed);
+      z.t_out.fetch_add(ns(t_done - t_waited), std::memory_order_relaxed);
+    }
     return rc;
   }
 
@@ -2451,6 +2601,7 @@ bool server_enabled() {
 
 int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
                  const std::vector<int> &out_ids, const void *image, int kind) {
+  if (ZcStats::on()) tl_zc_t0 = std::chrono::steady_clock::now();
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
   hipStream_t st = thread_stream();
@@ -2587,9 +2738,20 @@ int run_direct(PlanExt *e, char **ptrs, long long C, const std::vector<int> &in_
 std::mutex g_devs_mu;
 std::vector<int> g_host_devs;  // empty: the caller's current device
 
-std::vector<int> host_devices() {
-  std::lock_guard<std::mutex> lk(g_devs_mu);
-  return g_host_devs;
+std::atomic<unsigned> g_devs_version{0};  // bumped under g_devs_mu by every change
+
+// the device set, as a per-thread copy refreshed only when lsec_set_host_devices changed it
+// (no lock on the per-stripe path)
+const std::vector<int> &host_devices() {
+  thread_local std::vector<int> mine;
+  thread_local unsigned seen = ~0u;
+  const unsigned v = g_devs_version.load(std::memory_order_acquire);
+  if (v != seen) {
+    std::lock_guard<std::mutex> lk(g_devs_mu);
+    mine = g_host_devs;
+    seen = g_devs_version.load(std::memory_order_relaxed);
+  }
+  return mine;
 }
 
 struct DeviceGuard {
@@ -2635,6 +2797,7 @@ int on_host_devices(int nstripes, size_t bytes, F &&fn) {
 }
 
 int encode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C) {
+  PtrMemo memo;
   lio_erasure_plan_t *p = &e->pub;
   if (!ptrs) return fail("ptrs is NULL");
   if (check_geometry(p, C)) return -1;
@@ -2663,6 +2826,7 @@ int encode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C) {
 }
 
 int decode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C, const int *erasures) {
+  PtrMemo memo;
   lio_erasure_plan_t *p = &e->pub;
   if (!ptrs) return fail("ptrs is NULL");
   std::vector<int> ids;
@@ -2795,6 +2959,7 @@ int retry_direct(PlanExt *e, char **ptr, long long C, const std::vector<int> &id
 }
 
 void fp_encode_block(lio_erasure_plan_t *p, char **ptr, int block_size) {
+  if (ZcStats::on()) tl_call_t0 = std::chrono::steady_clock::now();
   PlanExt *e = ext_of(p);
   if (!e) {
     fprintf(stderr, "lstore_ec: encode_block on a plan not created by this library\n");
@@ -2810,6 +2975,7 @@ void fp_encode_block(lio_erasure_plan_t *p, char **ptr, int block_size) {
 }
 
 int fp_decode_block(lio_erasure_plan_t *p, char **ptr, int block_size, int *erasures) {
+  if (ZcStats::on()) tl_call_t0 = std::chrono::steady_clock::now();
   PlanExt *e = ext_of(p);
   if (!e) return fail("not an lstore_ec plan");
   if (decode_stripes_impl(e, ptr, 1, block_size, erasures) == 0) return 0;
@@ -3509,6 +3675,7 @@ int lsec_set_host_devices(const int *devices, int n) {
   }
   std::lock_guard<std::mutex> lk(g_devs_mu);
   g_host_devs.swap(v);
+  g_devs_version.fetch_add(1, std::memory_order_release);
   return 0;
 }
 

@@ -488,6 +488,24 @@ def test_device_pointers_through_fn_pointer(cuda):
         assert torch.equal(data[2], keep)
 
 
+def test_mixed_device_and_host_pointers_refused(cuda):
+    """A stripe whose chunk pointers mix device and host memory is refused with a status
+    (device-first: every chunk checked; host-first: the last chunk checked), not launched."""
+    import torch
+
+    from lstore_amd import erasure as E
+
+    k, m, size = 6, 3, 1 << 12
+    dev = torch.zeros((k + m, size), dtype=torch.uint8, device=cuda)
+    host = np.zeros((k + m, size), dtype=np.uint8)
+    with L.Plan.for_chunk(L.REED_SOL_VAN, k, m, size) as p:
+        dptr = [dev[i].data_ptr() for i in range(k + m)]
+        hptr = [host[i].ctypes.data for i in range(k + m)]
+        for ptrs in (dptr[:4] + hptr[4:], dptr[:-1] + hptr[-1:], hptr[:-1] + dptr[-1:]):
+            with pytest.raises(E.ErasureError, match="mix device and host"):
+                p.encode_stripes_ptrs(L.Plan._ptr_array(ptrs), 1, size)
+
+
 # ---------------------------------------------------------------- full-size, size-independent properties
 def test_full_size_roundtrip_and_linearity(cuda):
     import torch
