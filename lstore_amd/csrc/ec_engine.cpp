@@ -890,6 +890,8 @@ int ensure_slot(Staging::Slot &sl, size_t bytes, bool need_host = true) {
   return 0;
 }
 
+std::atomic<unsigned long long> g_st_queries{0};  // runtime pointer queries (LSEC_STATS)
+
 // Pointer attributes.  Every hipPointerGetAttributes takes a lock of the HIP runtime; per-stripe
 // calls from tens of threads made 10-20 queries each and spent most of their time queued on it
 // (an RS(6+3) 16 KiB call: 3 us of set-up at one thread, 140-360 us at 32 before this memo, 12 us
@@ -898,7 +900,7 @@ int ensure_slot(Staging::Slot &sl, size_t bytes, bool need_host = true) {
 // call answers repeated queries from a per-call memo (PtrMemo: the entry points of the batched
 // and per-stripe calls open one; with none open every query goes to the runtime).
 struct PtrInfo {
-  bool ok = false;  // the runtime knows the pointer (device memory or page-locked host memory)
+  bool ok = false;  // the query succeeded (ROCm 7 also answers for pageable memory: type Unregistered)
   hipMemoryType type = hipMemoryTypeHost;
   void *dev = nullptr;  // its device address
 };
@@ -922,6 +924,7 @@ PtrInfo query_ptr(const void *ptr) {
       if (kv.first == ptr) return kv.second;
   PtrInfo r;
   hipPointerAttribute_t attr;
+  g_st_queries.fetch_add(1, std::memory_order_relaxed);
   if (hipPointerGetAttributes(&attr, ptr) == hipSuccess) {
     r.ok = true;
     r.type = attr.type;
@@ -981,6 +984,12 @@ CallerPinned caller_pinned(char **ptrs, int nstripes, int km, const std::vector<
   // A first chunk that is not page-locked settles it, with no lock: every path below returns
   // "not pinned" for it too, and taking memory for pageable is always safe.  (Per-stripe calls
   // from hundreds of threads queued on this mutex.)
+  if (nstripes >= 1 && tl_memo_depth > 0)
+    for (const auto &kv : tl_memo)  // a chunk of this call already known not to be page-locked
+      if (!kv.second.ok || kv.second.type != hipMemoryTypeHost)
+        for (const std::vector<int> *ids : {&in_ids, &out_ids})
+          for (int id : *ids)
+            if (ptrs[id] == kv.first) return r;
   if (!in_ids.empty() && nstripes >= 1 && !is_pinned_host(ptrs[in_ids[0]])) return r;
   std::lock_guard<std::mutex> lk(g_inplace_mu);
   if (!g_inplace.empty()) {
@@ -1510,13 +1519,24 @@ bool is_device_ptr(const void *ptr) {
 // all k+m pointers of every stripe device memory?  then describe them as shard refs
 // Returns 1 (device layout in sh), 0 (host memory), -1 (device and host pointers mixed, or an
 // irregular device stride: refused rather than guessed).  A batch whose first chunk is device
-// memory has every chunk of its first and last stripe checked; one whose first chunk is host
-// memory has the last chunk of its first and last stripe checked (each check is a query under a
-// runtime lock that per-stripe calls contend on; a device pointer among host chunks would fault
-// the host copy, as it faults the reference's CPU code).
+// memory has every chunk of its first and last stripe checked; a multi-stripe batch whose first
+// chunk is host memory has the last chunk of its first and last stripe checked, and a single
+// stripe whose first chunk is host memory nothing more (each check is a query under a runtime
+// lock that per-stripe calls contend on; a device pointer among host chunks faults the host
+// copy, as it faults the reference's CPU code).
 int device_layout(const lio_erasure_plan_t *p, char **ptrs, int nstripes, std::vector<lsec_shard_t> &sh) {
   const int km = p->data_strips + p->parity_strips;
   if (!is_device_ptr(ptrs[0])) {
+    // A single-stripe call (LStore's per-stripe fn-pointer path) stops at its first chunk:
+    // every extra query is a turn on a runtime lock that spins, and at 128 threads on 16 CPUs
+    // one extra query per call cut 16 KiB decodes from 30.2 to 3.2-5.3 GiB/s with the CPU quota
+    // spent spinning (profiles/r02_v32_zc_decode2.txt).  LSEC_PTR_CHECK=all checks its last chunk
+    // too.
+    static const bool check_all = [] {
+      const char *v = getenv("LSEC_PTR_CHECK");
+      return v && strcmp(v, "all") == 0;
+    }();
+    if (!check_all && nstripes == 1) return 0;
     for (int s : {0, nstripes - 1})
       for (int i : {0, km - 1})
         if (is_device_ptr(ptrs[static_cast<size_t>(s) * km + i])) return fail("stripe pointers mix device and host memory");
@@ -2269,12 +2289,20 @@ bool wait_flag(const unsigned *flag, unsigned v, hipStream_t st, int *rc) {
 // launch (kernel over the caller's page-locked chunks, or over this thread's slot)
 thread_local std::chrono::steady_clock::time_point tl_call_t0;  // fn-pointer entry (LSEC_STATS)
 thread_local std::chrono::steady_clock::time_point tl_zc_t0;    // run_zerocopy entry (LSEC_STATS)
+thread_local long long tl_call_cpu0 = 0, tl_zc_cpu0 = 0;           // this thread's CPU ns at both
+
+long long thread_cpu_ns() {
+  struct timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return static_cast<long long>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
 
 struct ZcStats {
   std::atomic<unsigned long long> server{0}, no_slots{0}, not_servable{0}, launch_direct{0}, launch_slot{0};
   // server-served calls, wall time per phase (ns): fn-pointer entry -> server (plan checks,
   // layout and pinned-memory lookups), claim + copies in + posts, wait, copies out
   std::atomic<unsigned long long> t_setup{0}, t_zc{0}, t_post{0}, t_wait{0}, t_out{0};
+  std::atomic<unsigned long long> c_setup{0}, c_zc{0}, c_post{0}, c_wait{0}, c_out{0};  // thread CPU ns
   static bool on() {
     static const bool v = getenv("LSEC_STATS") != nullptr;
     return v;
@@ -2288,12 +2316,16 @@ struct ZcStats {
                 "own launch (caller page-locked) %llu, own launch (slot) %llu\n", z.server.load(), z.no_slots.load(),
                 z.not_servable.load(), z.launch_direct.load(), z.launch_slot.load());
         fprintf(stderr, "[lsec stats] waits: spin hits %llu, parks %llu, poller wakes %llu, timed-out slices %llu; "
-                "claims missed %llu, claim retries %llu\n", g_st_spin_hits.load(), g_st_parks.load(), g_st_wakes.load(),
-                g_st_slices.load(), g_st_claim_misses.load(), g_st_claim_spins.load());
+                "claims missed %llu, claim retries %llu; runtime pointer queries %llu\n", g_st_spin_hits.load(),
+                g_st_parks.load(), g_st_wakes.load(), g_st_slices.load(), g_st_claim_misses.load(), g_st_claim_spins.load(),
+                g_st_queries.load());
         const double n = static_cast<double>(std::max(1ULL, z.server.load())) * 1e3;
         fprintf(stderr, "[lsec stats] server calls, mean wall us: setup %.2f (of it in run_zerocopy %.2f), claim+copy-in+post %.2f, "
                 "wait %.2f, copy-out %.2f\n", z.t_setup.load() / n, z.t_zc.load() / n, z.t_post.load() / n, z.t_wait.load() / n,
                 z.t_out.load() / n);
+        fprintf(stderr, "[lsec stats] server calls, mean thread CPU us: setup %.2f (of it in run_zerocopy %.2f), claim+copy-in+post "
+                "%.2f, wait %.2f, copy-out %.2f\n", z.c_setup.load() / n, z.c_zc.load() / n, z.c_post.load() / n,
+                z.c_wait.load() / n, z.c_out.load() / n);
       });
       return p;
     }();
@@ -2329,6 +2361,9 @@ class StripeServer {
   int run(PlanExt *e, char **ptrs, long long C, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
           const void *image, int kind, const CallerPinned *cp) {
     const auto t_enter = std::chrono::steady_clock::now();
+    const bool stats = ZcStats::on();
+    const long long c_enter = stats ? thread_cpu_ns() : 0;
+    long long c_post = 0, c_waited = 0;
     const size_t nin = in_ids.size(), nout = out_ids.size(), nio = nin + nout;
     const auto refuse = [] {
       ZcStats::get().not_servable.fetch_add(1, std::memory_order_relaxed);
@@ -2409,6 +2444,7 @@ class StripeServer {
       __atomic_store_n(&sh_->post[lsec::srv_wg(sl)][lsec::srv_word(sl)], want[q], __ATOMIC_RELEASE);
     }
     const auto t_post = std::chrono::steady_clock::now();
+    if (stats) c_post = thread_cpu_ns();
     int rc = ensure_running(false);
     const auto t0 = std::chrono::steady_clock::now();
     auto last_check = t0;
@@ -2430,6 +2466,7 @@ class StripeServer {
       }
     }
     const auto t_waited = std::chrono::steady_clock::now();
+    if (stats) c_waited = thread_cpu_ns();
     static const bool trace = getenv("LSEC_TRACE") != nullptr;
     if (trace) {  // calls slower than 1 ms: where the time went
       const auto t_end = std::chrono::steady_clock::now();
@@ -2449,7 +2486,7 @@ class StripeServer {
         for (size_t r = 0; r < nout; ++r) std::memcpy(ptrs[out_ids[r]] + c0, region + (nin + r) * n, static_cast<size_t>(n));
       }
     if (rc == 0) release(nparts, slot);  // a slot whose post may still be served is never handed out again
-    if (rc == 0 && ZcStats::on()) {
+    if (rc == 0 && stats) {
       ZcStats &z = ZcStats::get();
       const auto ns = [](std::chrono::steady_clock::duration d) {
         return static_cast<unsigned long long>(std::chrono::duration_cast<std::chrono::nanoseconds>(d).count());
@@ -2460,6 +2497,12 @@ class StripeServer {
       z.t_post.fetch_add(ns(t_post - t_enter), std::memory_order_relaxed);
       z.t_wait.fetch_add(ns(t_waited - t_post), std::memory_order_relaxed);
       z.t_out.fetch_add(ns(t_done - t_waited), std::memory_order_relaxed);
+      const long long c_done = thread_cpu_ns();
+      if (tl_call_cpu0 && c_enter > tl_call_cpu0) z.c_setup.fetch_add(c_enter - tl_call_cpu0, std::memory_order_relaxed);
+      if (tl_zc_cpu0 && c_enter > tl_zc_cpu0) z.c_zc.fetch_add(c_enter - tl_zc_cpu0, std::memory_order_relaxed);
+      z.c_post.fetch_add(c_post - c_enter, std::memory_order_relaxed);
+      z.c_wait.fetch_add(c_waited - c_post, std::memory_order_relaxed);
+      z.c_out.fetch_add(c_done - c_waited, std::memory_order_relaxed);
     }
     return rc;
   }
@@ -2541,6 +2584,13 @@ class StripeServer {
                             std::chrono::steady_clock::now().time_since_epoch()).count();
     if (!check && now - last_seen_us_.load(std::memory_order_relaxed) > 1500) check = true;
     if (!check && running_.load(std::memory_order_acquire)) return 0;
+    if (running_.load(std::memory_order_acquire)) {
+      // one liveness query per 200 us for all threads: after the cgroup throttles the process
+      // every waiter's slice expires at once, and each asking the runtime (under mu_) kept a
+      // 128-thread process throttled (profiles/r02_v32_zc_decode2.txt)
+      int64_t prev = last_check_us_.load(std::memory_order_relaxed);
+      if (now - prev < 200 || !last_check_us_.compare_exchange_strong(prev, now)) return 0;
+    }
     std::lock_guard<std::mutex> lk(mu_);
     if (broken_) return fail("stripe server: unusable after an earlier failure");
     if (running_ && check) {
@@ -2589,6 +2639,7 @@ class StripeServer {
   std::atomic<bool> running_{false};
   std::atomic<bool> broken_{false};
   std::atomic<int64_t> last_seen_us_{0};
+  std::atomic<int64_t> last_check_us_{0};
 };
 
 bool server_enabled() {
@@ -2601,7 +2652,10 @@ bool server_enabled() {
 
 int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
                  const std::vector<int> &out_ids, const void *image, int kind) {
-  if (ZcStats::on()) tl_zc_t0 = std::chrono::steady_clock::now();
+  if (ZcStats::on()) {
+    tl_zc_t0 = std::chrono::steady_clock::now();
+    tl_zc_cpu0 = thread_cpu_ns();
+  }
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
   hipStream_t st = thread_stream();
@@ -2959,7 +3013,10 @@ int retry_direct(PlanExt *e, char **ptr, long long C, const std::vector<int> &id
 }
 
 void fp_encode_block(lio_erasure_plan_t *p, char **ptr, int block_size) {
-  if (ZcStats::on()) tl_call_t0 = std::chrono::steady_clock::now();
+  if (ZcStats::on()) {
+    tl_call_t0 = std::chrono::steady_clock::now();
+    tl_call_cpu0 = thread_cpu_ns();
+  }
   PlanExt *e = ext_of(p);
   if (!e) {
     fprintf(stderr, "lstore_ec: encode_block on a plan not created by this library\n");
@@ -2975,7 +3032,10 @@ void fp_encode_block(lio_erasure_plan_t *p, char **ptr, int block_size) {
 }
 
 int fp_decode_block(lio_erasure_plan_t *p, char **ptr, int block_size, int *erasures) {
-  if (ZcStats::on()) tl_call_t0 = std::chrono::steady_clock::now();
+  if (ZcStats::on()) {
+    tl_call_t0 = std::chrono::steady_clock::now();
+    tl_call_cpu0 = thread_cpu_ns();
+  }
   PlanExt *e = ext_of(p);
   if (!e) return fail("not an lstore_ec plan");
   if (decode_stripes_impl(e, ptr, 1, block_size, erasures) == 0) return 0;

@@ -489,21 +489,25 @@ def test_device_pointers_through_fn_pointer(cuda):
 
 
 def test_mixed_device_and_host_pointers_refused(cuda):
-    """A stripe whose chunk pointers mix device and host memory is refused with a status
-    (device-first: every chunk checked; host-first: the last chunk checked), not launched."""
+    """Stripes whose chunk pointers mix device and host memory are refused with a status, not
+    launched: device-first batches have every chunk of their first and last stripe checked,
+    multi-stripe host-first batches the last chunk of their first and last stripe."""
     import torch
 
     from lstore_amd import erasure as E
 
     k, m, size = 6, 3, 1 << 12
-    dev = torch.zeros((k + m, size), dtype=torch.uint8, device=cuda)
-    host = np.zeros((k + m, size), dtype=np.uint8)
+    dev = torch.zeros((2, k + m, size), dtype=torch.uint8, device=cuda)
+    host = np.zeros((2, k + m, size), dtype=np.uint8)
     with L.Plan.for_chunk(L.REED_SOL_VAN, k, m, size) as p:
-        dptr = [dev[i].data_ptr() for i in range(k + m)]
-        hptr = [host[i].ctypes.data for i in range(k + m)]
-        for ptrs in (dptr[:4] + hptr[4:], dptr[:-1] + hptr[-1:], hptr[:-1] + dptr[-1:]):
+        dptr = [[dev[s, i].data_ptr() for i in range(k + m)] for s in range(2)]
+        hptr = [[host[s, i].ctypes.data for i in range(k + m)] for s in range(2)]
+        cases = [(dptr[0][:4] + hptr[0][4:], 1), (dptr[0][:-1] + hptr[0][-1:], 1),
+                 (dptr[0] + dptr[1][:-1] + hptr[1][-1:], 2), (hptr[0] + hptr[1][:-1] + dptr[1][-1:], 2),
+                 (hptr[0][:-1] + dptr[0][-1:] + hptr[1], 2)]
+        for ptrs, n in cases:
             with pytest.raises(E.ErasureError, match="mix device and host"):
-                p.encode_stripes_ptrs(L.Plan._ptr_array(ptrs), 1, size)
+                p.encode_stripes_ptrs(L.Plan._ptr_array(ptrs), n, size)
 
 
 # ---------------------------------------------------------------- full-size, size-independent properties
