@@ -13,6 +13,7 @@ run X=default
 run LSEC_WAIT_SPINNERS=0
 run LSEC_WAIT_ADAPT=0 LSEC_WAIT_SPINNERS=0
 run LSEC_WAIT_POLLERS=1
+run LSEC_PTR_CHECK=first
 run X=default
 echo "== encode default" >> $out
 LSEC_STATS=1 timeout -k 10 60 build/fnptr_bench 16384 128 2 cauchy_good encode >> $out 2>&1 || exit 1
