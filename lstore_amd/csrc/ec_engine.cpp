@@ -3781,4 +3781,71 @@ int lsec_hbm_mix_dev(const lsec_shard_t *shards, int k, int m, int nstripes, lon
   return 0;
 }
 
+// Self-test of the completion waits (FlagWaits: spinners, lock-free parking, pollers) with the
+// flags written by host threads instead of the GPU: `threads` waiters, each with a producer that
+// sets its 1..16 flags in random order after a random delay of 0-300 us, `iters` rounds.  Every
+// wait must end with all its flags set and within 2 s.  Test hook, not part of include/*.h;
+// needs no GPU.  Returns 0, or -1 with a message.
+int lsec_selftest_waits(int threads, int iters) {
+  if (threads < 1 || threads > 512 || iters < 1) return fail("lsec_selftest_waits: bad arguments");
+  struct alignas(64) Pair {
+    unsigned flags[16][16];  // one 64-byte line per flag, as the server's done lines
+    std::atomic<int> ready{-1};
+    int n = 1;
+  };
+  std::vector<std::unique_ptr<Pair>> pairs;
+  for (int t = 0; t < threads; ++t) {
+    pairs.emplace_back(new Pair());
+    std::memset(pairs.back()->flags, 0, sizeof(pairs.back()->flags));
+    pairs.back()->n = 1 + (t * 7) % 16;
+  }
+  std::atomic<int> bad{0};
+  const unsigned long long parks0 = g_st_parks.load(), wakes0 = g_st_wakes.load();
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; ++t) {
+    th.emplace_back([&, t] {  // producer
+      Pair &p = *pairs[t];
+      uint64_t x = 0x9E3779B97F4A7C15ull * (t + 1);
+      for (int it = 0; it < iters && !bad.load(); ++it) {
+        while (p.ready.load(std::memory_order_acquire) < it && !bad.load()) std::this_thread::yield();
+        x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+        std::this_thread::sleep_for(std::chrono::microseconds(x % 300));
+        int order[16];
+        for (int i = 0; i < p.n; ++i) order[i] = i;
+        for (int i = p.n - 1; i > 0; --i) std::swap(order[i], order[(x >> (i % 48)) % (i + 1)]);
+        for (int i = 0; i < p.n; ++i) __atomic_store_n(&p.flags[order[i]][0], static_cast<unsigned>(it + 1), __ATOMIC_RELEASE);
+      }
+    });
+    th.emplace_back([&, t] {  // waiter
+      Pair &p = *pairs[t];
+      const unsigned *f[16];
+      unsigned want[16];
+      for (int i = 0; i < p.n; ++i) f[i] = &p.flags[i][0];
+      for (int it = 0; it < iters && !bad.load(); ++it) {
+        for (int i = 0; i < p.n; ++i) want[i] = static_cast<unsigned>(it + 1);
+        p.ready.store(it, std::memory_order_release);
+        const auto t0 = std::chrono::steady_clock::now();
+        while (!FlagWaits::get().wait(f, want, p.n, std::chrono::microseconds(500))) {
+          if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+            bad.store(1);
+            return;
+          }
+        }
+        for (int i = 0; i < p.n; ++i)
+          if (static_cast<int>(__atomic_load_n(f[i], __ATOMIC_ACQUIRE) - want[i]) < 0) {
+            bad.store(2);
+            return;
+          }
+      }
+    });
+  }
+  for (auto &x : th) x.join();
+  if (bad.load() == 1) return fail("lsec_selftest_waits: a wait did not end within 2 s of its flags");
+  if (bad.load() == 2) return fail("lsec_selftest_waits: a wait returned before all its flags were set");
+  // delays up to 300 us against a 30 us spin: long runs must have parked and been woken
+  if (static_cast<long long>(threads) * iters >= 200 && (g_st_parks.load() == parks0 || g_st_wakes.load() == wakes0))
+    return fail("lsec_selftest_waits: no waiter parked or was woken by a poller");
+  return 0;
+}
+
 }  // extern "C"
