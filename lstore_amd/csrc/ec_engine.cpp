@@ -2729,11 +2729,34 @@ bool zerocopy_enabled() {
 
 // host-memory batches: small ones are served zero-copy by the calling thread (or coalesced
 // with concurrent callers), large ones stream through their own staging pipeline
+//
+// Between the zero-copy and coalescing limits (LStore's 1 MiB chunks: 9 MiB per RS(6+3)
+// stripe), a call of at least 4 MiB takes its own pipeline (in-place pinned from 8 MiB, else
+// packed on the copy pool) while few
+// such calls run at once: no packing copies (RS(6+3) 1 MiB encode at one thread 15 -> 27 GiB/s,
+// Cauchy at 8 threads 19-23 -> 35-36); with many, the registrations contend on the runtime and
+// the dispatcher's packed batches win (decode at 32 threads 38 vs 17 GiB/s;
+// profiles/r02_v36_route_1m.jsonl; gated vs dispatcher-only in r02_v36_route_1m2.jsonl).
 int run_host_auto(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
                   const std::vector<int> &out_ids, const void *image, int kind) {
   const size_t bytes = static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()) * C;
   if (zerocopy_enabled() && bytes <= zerocopy_limit()) return run_zerocopy(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
-  if (bytes <= coalesce_limit()) return run_coalesced(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
+  if (bytes <= coalesce_limit()) {
+    static std::atomic<int> own_inflight{0};
+    static const int own_max = [] {  // LSEC_OWN_PIPELINE_MAX: A/B runs (0: always the dispatcher)
+      const char *v = getenv("LSEC_OWN_PIPELINE_MAX");
+      return v ? std::max(0, atoi(v)) : std::max(2, usable_cpus() / 2);
+    }();
+    if (bytes >= (4u << 20) && own_max > 0) {
+      if (own_inflight.fetch_add(1, std::memory_order_acq_rel) < own_max) {
+        const int rc = run_host(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
+        own_inflight.fetch_sub(1, std::memory_order_acq_rel);
+        return rc;
+      }
+      own_inflight.fetch_sub(1, std::memory_order_acq_rel);
+    }
+    return run_coalesced(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
+  }
   return run_host(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
 }
 
