@@ -932,7 +932,7 @@ PtrInfo query_ptr(const void *ptr) {
   } else {
     (void)hipGetLastError();  // pageable host memory reports an error on some runtimes
   }
-  if (tl_memo_depth > 0 && tl_memo.size() < 1024) tl_memo.push_back({ptr, r});
+  if (tl_memo_depth > 0 && tl_memo.size() < 64) tl_memo.push_back({ptr, r});  // small: scanned linearly
   return r;
 }
 
@@ -1048,12 +1048,13 @@ class InPlacePin {
     if (total < kMinBytes) return false;  // packing a small batch is cheaper than the syscalls
     // Each DMA from registered pageable memory has a fixed cost on top of the bytes, so pin
     // only when the copies the pinned path will issue (one per run of host-contiguous chunks,
-    // stripe by stripe) average >= 768 KiB; smaller runs pack faster.  Measured A/B of the
-    // threshold (tools/pin_run_ab.py, profiles/r02_v27_pin_run_ab.jsonl): runs of 896 KiB and
-    // up pin faster (RS(6+3) C = 256 KiB decode 30 -> 35 GiB/s, C = 512 KiB 28 -> 41, C = 1 MiB
-    // decode 31 -> 46; RS(10+4) C = 128 KiB encode 29 -> 31), 704 KiB ties and 576 KiB and
-    // below pack faster (RS(6+3) C = 64 KiB encode 26 vs 17).  Round 1's 4 MiB threshold had
-    // every decode below C = 2 MiB packing.
+    // stripe by stripe) average >= 2.5 MiB; smaller runs pack faster.  Round 1's 4 MiB had
+    // every single-erasure decode below C = 2 MiB packing (RS(6+3) 1 MiB decode: 3.5 MiB runs,
+    // 31 GiB/s packed, 37-46 pinned).  An in-process A/B (tools/pin_run_ab.py,
+    // profiles/r02_v27_pin_run_ab.jsonl) put the break-even near 800 KiB, but the c5 sweep
+    // with that threshold (r02_v38_sweep_c5.jsonl vs r02_v25) lost up to half the rate at
+    // 1.5-2.25 MiB runs (RS(6+3) 256 KiB encode 32 -> 16, 512 KiB 29 -> 22.5) while runs of
+    // 2.75 MiB and up gained (RS(10+4) 512 KiB decode 30 -> 40).
     size_t runs = 0;
     for (const std::vector<int> *ids : {&in_ids, &out_ids}) {
       const char *end = nullptr;
@@ -1129,7 +1130,7 @@ class InPlacePin {
  private:
   static constexpr size_t kMaxRegions = 1024;
   static constexpr size_t kMinBytes = 8ull << 20;
-  static constexpr size_t kMinRun = 768ull << 10;
+  static constexpr size_t kMinRun = 2560ull << 10;
   // LSEC_PIN_MIN_RUN_KB overrides kMinRun (read per call: measurement A/B runs)
   static size_t min_run() {
     const char *s = getenv("LSEC_PIN_MIN_RUN_KB");
