@@ -6,6 +6,9 @@ bit-exactly against the oracle from many threads at once, across the server's id
 and relaunch, with ragged chunk sizes, and across plans whose coefficient images reuse device
 addresses while the server runs.
 """
+import json
+import os
+import subprocess
 import threading
 import time
 
@@ -98,3 +101,25 @@ def test_new_plans_while_the_server_runs(cuda):
             sh[:k] = rng.integers(0, 256, (k, C), dtype=np.uint8)
             p.encode_block([sh[i] for i in range(k + m)])
             assert np.array_equal(sh[k:], O.encode(method, np.ascontiguousarray(sh[:k]), m, p.packet_size)), round_
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "build", "fnptr_bench")
+REF = os.path.join(ROOT, "oracle", "_ref", "libjerasure_ref.so")
+
+
+@pytest.mark.skipif(not (os.path.exists(BENCH) and os.path.exists(REF)), reason="build/fnptr_bench or oracle/_ref not built")
+@pytest.mark.parametrize("chunk,threads,method,op,pinned", [
+    (16384, 128, "reed_sol_van", "encode", 0), (16384, 128, "cauchy_good", "decode", 0),
+    (65536, 64, "cauchy_good", "encode", 1), (1 << 20, 16, "reed_sol_van", "encode", 0)])
+def test_fn_pointer_stress_bit_exact(cuda, chunk, threads, method, op, pinned):
+    """LStore's pattern in C (tools/fnptr_bench.c, FNPTR_VERIFY=1): every thread calls
+    encode_block / decode_block on its own stripe for 1 s; before each call the chunks it must
+    write are overwritten, after it they must equal the reference's (oracle/_ref) -- every
+    call checked, at up to 128 threads (server slots, parking, one pointer query per call)."""
+    env = dict(os.environ, FNPTR_VERIFY="1", FNPTR_REF=REF, FNPTR_PINNED=str(pinned))
+    out = subprocess.run([BENCH, str(chunk), str(threads), "1", method, op], env=env, capture_output=True,
+                         text=True, timeout=100)
+    assert out.returncode == 0, (out.returncode, out.stdout[-500:], out.stderr[-500:])
+    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    assert rec["verified"] > 0 and rec["mismatches"] == 0, rec

@@ -21,6 +21,10 @@
  *        FNPTR_REF=path  also time the reference: oracle/_ref/libjerasure_ref.so (test
  *                        infrastructure: the real jerasure behind erasure_tools.c's dispatch)
  *        FNPTR_ONLY_REF=1  time the reference only
+ *        FNPTR_VERIFY=1  (with FNPTR_REF) every timed engine call is checked: the chunks it writes
+ *                        are overwritten before the call, and after it must equal the reference's
+ *                        (parity for encode, the lost data chunk 0 for decode); the JSON line then
+ *                        carries "verified" and "mismatches", and the exit status is 2 on any
  */
 #include <dlfcn.h>
 #include <pthread.h>
@@ -40,7 +44,8 @@ static void (*g_ref_encode)(void *, char **, int);
 static int (*g_ref_decode)(void *, char **, int, int *);
 static int (*g_host_malloc)(void **, size_t, unsigned);
 static int (*g_host_free)(void *);
-static int g_chunk, g_decode, g_use_ref, g_k = 6, g_m = 3;
+static int g_chunk, g_decode, g_use_ref, g_verify, g_k = 6, g_m = 3;
+static long g_verified, g_mismatch;  /* FNPTR_VERIFY counters (atomic adds) */
 static double g_seconds;
 static volatile double g_t_end;
 static pthread_barrier_t g_bar;
@@ -82,18 +87,33 @@ static void *worker(void *arg)
     }
     char *ptr[256];
     int erasures[2] = {0, -1};
+    char *gold = NULL;  /* FNPTR_VERIFY: the stripe with the reference's parity */
+    const size_t C = (size_t)g_chunk;
     if (buf) {
         for (size_t i = 0; i < (size_t)(k + m) * g_chunk; i++) buf[i] = (char)(i * 131 + r->t);
         for (int i = 0; i < k + m; i++) ptr[i] = buf + (size_t)i * g_chunk;
-        if (g_use_ref) g_ref_encode(g_ref, ptr, g_chunk);   /* consistent parity for the decodes */
+        if (g_use_ref || g_verify) g_ref_encode(g_ref, ptr, g_chunk);   /* consistent parity for the decodes */
         else g_plan->encode_block(g_plan, ptr, g_chunk);
+        if (g_verify && !g_use_ref) {
+            gold = malloc((size_t)(k + m) * C);
+            if (gold) memcpy(gold, buf, (size_t)(k + m) * C);
+        }
         for (int c = 0; c < 3; c++) one_call(ptr, erasures);  /* warm */
     }
     pthread_barrier_wait(&g_bar);  /* timed phase starts */
     while (buf) {
+        if (gold) {  /* overwrite what the call must write */
+            if (g_decode) memset(ptr[0], 0xA5, C);
+            else memset(ptr[k], 0x5A, (size_t)m * C);
+        }
         double t0 = now();
         one_call(ptr, erasures);
         double t1 = now();
+        if (gold) {
+            const int bad = g_decode ? memcmp(ptr[0], gold, C) != 0 : memcmp(ptr[k], gold + (size_t)k * C, (size_t)m * C) != 0;
+            __atomic_add_fetch(&g_verified, 1, __ATOMIC_RELAXED);
+            if (bad) __atomic_add_fetch(&g_mismatch, 1, __ATOMIC_RELAXED);
+        }
         if (r->nlat < MAX_SAMPLES) r->lat[r->nlat++] = t1 - t0;
         r->calls++;
         if (t1 >= g_t_end) break;
@@ -103,6 +123,7 @@ static void *worker(void *arg)
         if (g_host_malloc) g_host_free(buf);
         else free(buf);
     }
+    free(gold);
     return NULL;
 }
 
@@ -172,11 +193,12 @@ static void run(int T, const char *impl, const char *method)
     printf("{\"impl\": \"%s\", \"op\": \"%s\", \"chunk\": %d, \"threads\": %d, \"calls\": %ld, \"seconds\": %.3f, "
            "\"method\": \"%s\", \"pinned\": %d, \"small_path\": \"%s\", \"per_call_us_p50\": %.1f, "
            "\"per_call_us_p99\": %.1f, \"per_call_us_p999\": %.1f, \"per_call_us_max\": %.1f, \"per_call_us_mean\": %.1f, "
-           "\"gibps\": %.3f, \"cpu_util\": %.2f, \"cpu_us_per_call\": %.1f, \"cgroup_throttled_ms\": %.1f}\n",
+           "\"gibps\": %.3f, \"cpu_util\": %.2f, \"cpu_us_per_call\": %.1f, \"cgroup_throttled_ms\": %.1f, "
+           "\"verified\": %ld, \"mismatches\": %ld}\n",
            impl, g_decode ? "decode" : "encode", g_chunk, T, calls, wall, method, g_host_malloc != NULL, sp ? sp : "default",
            n ? lat[n / 2] * 1e6 : 0.0, n ? lat[(size_t)(n * 0.99)] * 1e6 : 0.0, n ? lat[(size_t)(n * 0.999)] * 1e6 : 0.0,
            n ? lat[n - 1] * 1e6 : 0.0, n ? sum / n * 1e6 : 0.0, calls * (double)g_k * g_chunk / wall / (1 << 30),
-           cpu / wall, calls ? cpu / calls * 1e6 : 0.0, thr * 1e3);
+           cpu / wall, calls ? cpu / calls * 1e6 : 0.0, thr * 1e3, g_verified, g_mismatch);
     fflush(stdout);
     free(lat);
 }
@@ -207,8 +229,8 @@ int main(int argc, char **argv)
         return 1;
     }
     const char *only_ref = getenv("FNPTR_ONLY_REF");
-    if (!(only_ref && atoi(only_ref))) run(T, "engine", JE_method[method]);
     const char *ref_so = getenv("FNPTR_REF");
+    g_verify = getenv("FNPTR_VERIFY") && atoi(getenv("FNPTR_VERIFY"));
     if (ref_so && *ref_so) {
         void *h = dlopen(ref_so, RTLD_NOW | RTLD_LOCAL);
         void *(*ref_new)(int, int, int, int, int) = h ? (void *(*)(int, int, int, int, int))dlsym(h, "ref_plan_new") : NULL;
@@ -219,9 +241,16 @@ int main(int argc, char **argv)
             return 1;
         }
         g_ref = ref_new(method, g_k, g_m, g_plan->w, g_plan->packet_size);
+    } else if (g_verify) {
+        fprintf(stderr, "FNPTR_VERIFY needs FNPTR_REF\n");
+        return 1;
+    }
+    if (!(only_ref && atoi(only_ref))) run(T, "engine", JE_method[method]);
+    const int bad = g_verify && (g_mismatch > 0 || g_verified == 0);
+    if (g_ref && !g_verify) {
         g_use_ref = 1;
         run(T, "reference", JE_method[method]);
     }
     et_destroy_plan(g_plan);
-    return 0;
+    return bad ? 2 : 0;
 }
