@@ -1909,10 +1909,14 @@ int run_coalesced(PlanExt *e, char **ptrs, int nstripes, long long C, const std:
 // and writes that slot over PCIe directly (zero-copy): one launch on the thread's stream and
 // one synchronisation per call, no DMA and no other thread.  Chunks the caller already holds
 // in page-locked memory are read and written in place, with no copies at all.
-size_t zerocopy_limit() {  // per-call bytes (inputs + outputs) served this way; LSEC_ZEROCOPY_KB
+// Per-call bytes (inputs + outputs) served this way; LSEC_ZEROCOPY_KB.  4 MiB: calls of 1-4 MiB
+// (RS(6+3) at 128 / 256 KiB chunks) ran 1.3-2.5x faster zero-copy than through the dispatcher
+// at 1-128 threads (profiles/r02_v42_route_mid.jsonl).  Each thread keeps a page-locked slot as
+// large as its largest such call.
+size_t zerocopy_limit() {
   static size_t b = [] {
     const char *s = getenv("LSEC_ZEROCOPY_KB");
-    return static_cast<size_t>(std::max(0L, s ? atol(s) : 1024L)) << 10;
+    return static_cast<size_t>(std::max(0L, s ? atol(s) : 4096L)) << 10;
   }();
   return b;
 }
