@@ -968,8 +968,42 @@ bool inplace_overlaps_locked(uintptr_t lo, uintptr_t hi) {
 // in-place registrations first: a range a concurrent InPlacePin has claimed (it claims before
 // it registers and releases after it unregisters) is never taken for caller-pinned memory,
 // since its owner may unregister it while this call's DMA or copy kernel still reads it.
+// A page-locked allocation a call has verified: [lo, hi) host bytes, device alias = host + delta.
+// A chunk inside one needs no further runtime query (each takes a runtime lock; a page-locked
+// per-stripe call made ~11 of them under g_inplace_mu: RS(6+3) 16 KiB at 128 threads spent
+// 430 us of its 450 us in this set-up, profiles/r02_v45_zc_phases.txt).
+struct PinnedAlloc {
+  uintptr_t lo, hi;
+  intptr_t delta;
+};
+
+// p..p+len inside one page-locked allocation with a device alias?  (its device address in *dev)
+bool pinned_chunk(const char *p, size_t len, std::vector<PinnedAlloc> &seen, uint64_t *dev) {
+  const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+  for (const PinnedAlloc &a : seen)
+    if (u >= a.lo && u + len <= a.hi) {
+      *dev = static_cast<uint64_t>(static_cast<intptr_t>(u) + a.delta);
+      return true;
+    }
+  const PtrInfo i = query_ptr(p);
+  if (!i.ok || i.type != hipMemoryTypeHost || !i.dev) return false;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(const_cast<char *>(p))) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(base), hi = lo + size;
+  if (u < lo || u + len > hi) return false;
+  const intptr_t delta = reinterpret_cast<intptr_t>(i.dev) - static_cast<intptr_t>(u);
+  seen.push_back({lo, hi, delta});
+  *dev = reinterpret_cast<uint64_t>(i.dev);
+  return true;
+}
+
 bool caller_pinned_aliases(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids,
-                           const std::vector<int> &out_ids, long long C, std::vector<uint64_t> &dev);
+                           const std::vector<int> &out_ids, long long C, std::vector<PinnedAlloc> &seen,
+                           std::vector<uint64_t> &dev);
 
 struct CallerPinned {
   bool pinned = false, by_kernel = false;
@@ -1000,14 +1034,16 @@ CallerPinned caller_pinned(char **ptrs, int nstripes, int km, const std::vector<
           if (inplace_overlaps_locked(a & ~(kPage - 1), (a + static_cast<uintptr_t>(C) + kPage - 1) & ~(kPage - 1))) return r;
         }
   }
+  std::vector<PinnedAlloc> seen;
+  uint64_t d = 0;
   for (int s : {0, nstripes - 1}) {
     for (int id : in_ids)
-      if (!is_pinned_host(ptrs[static_cast<size_t>(s) * km + id])) return r;
+      if (!pinned_chunk(ptrs[static_cast<size_t>(s) * km + id], static_cast<size_t>(C), seen, &d)) return r;
     for (int id : out_ids)
-      if (!is_pinned_host(ptrs[static_cast<size_t>(s) * km + id])) return r;
+      if (!pinned_chunk(ptrs[static_cast<size_t>(s) * km + id], static_cast<size_t>(C), seen, &d)) return r;
   }
   r.pinned = true;
-  r.by_kernel = kernel_ok && caller_pinned_aliases(ptrs, nstripes, km, in_ids, out_ids, C, r.dev);
+  r.by_kernel = kernel_ok && caller_pinned_aliases(ptrs, nstripes, km, in_ids, out_ids, C, seen, r.dev);
   return r;
 }
 
@@ -1205,7 +1241,8 @@ bool kernel_transport_aligned(char **ptrs, int nstripes, int km, const std::vect
 // address of chunk i, in the order stripe, then in_ids, then out_ids.
 // (called by caller_pinned with g_inplace_mu held)
 bool caller_pinned_aliases(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids,
-                           const std::vector<int> &out_ids, long long C, std::vector<uint64_t> &dev) {
+                           const std::vector<int> &out_ids, long long C, std::vector<PinnedAlloc> &seen,
+                           std::vector<uint64_t> &dev) {
   size_t runs = 0, total = 0;
   for (const std::vector<int> *ids : {&in_ids, &out_ids}) {
     const char *end = nullptr;
@@ -1220,26 +1257,12 @@ bool caller_pinned_aliases(char **ptrs, int nstripes, int km, const std::vector<
   if (runs == 0 || total / runs >= (1ull << 20)) return false;
   dev.clear();
   dev.reserve(static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()));
-  uintptr_t lo = 1, hi = 0;  // last allocation seen [lo, hi)
   for (int s = 0; s < nstripes; ++s)
     for (const std::vector<int> *ids : {&in_ids, &out_ids})
       for (int id : *ids) {
-        char *p = ptrs[static_cast<size_t>(s) * km + id];
-        const PtrInfo a = query_ptr(p);
-        if (!a.ok || a.type != hipMemoryTypeHost || !a.dev) return false;
-        const uintptr_t u = reinterpret_cast<uintptr_t>(p);
-        if (u < lo || u + static_cast<uintptr_t>(C) > hi) {
-          hipDeviceptr_t base = nullptr;
-          size_t size = 0;
-          if (hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(p)) != hipSuccess) {
-            (void)hipGetLastError();
-            return false;
-          }
-          lo = reinterpret_cast<uintptr_t>(base);
-          hi = lo + size;
-          if (u < lo || u + static_cast<uintptr_t>(C) > hi) return false;
-        }
-        dev.push_back(reinterpret_cast<uint64_t>(a.dev));
+        uint64_t d = 0;
+        if (!pinned_chunk(ptrs[static_cast<size_t>(s) * km + id], static_cast<size_t>(C), seen, &d)) return false;
+        dev.push_back(d);
       }
   return true;
 }
@@ -2349,6 +2372,10 @@ struct ZcStats {
 class StripeServer {
  public:
   static StripeServer *for_device(int dev) {
+    // every per-stripe call asks: a lock-free read once the device's server exists
+    static std::atomic<StripeServer *> fast[64] = {};
+    if (dev >= 0 && dev < 64)
+      if (StripeServer *f = fast[dev].load(std::memory_order_acquire)) return f;
     static std::mutex m;
     static std::map<int, StripeServer *> all;  // intentionally leaked: lives until exit
     std::lock_guard<std::mutex> lk(m);
@@ -2359,6 +2386,7 @@ class StripeServer {
       static std::once_flag once;
       std::call_once(once, [] { atexit(stop_all); });
     }
+    if (dev >= 0 && dev < 64) fast[dev].store(r, std::memory_order_release);
     return r;
   }
 
