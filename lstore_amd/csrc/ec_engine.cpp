@@ -1956,6 +1956,16 @@ std::map<int, std::vector<SignalBlock>> &signal_pool() {
   return *p;
 }
 
+std::atomic<size_t> g_zc_slot_bytes{0};  // page-locked bytes of all threads' zero-copy slots
+
+size_t zc_slot_budget() {
+  static const size_t b = [] {
+    const char *s = getenv("LSEC_ZC_SLOTS_MB");
+    return static_cast<size_t>(std::max(0L, s ? atol(s) : 1024L)) << 20;
+  }();
+  return b;
+}
+
 struct ZcSlot {  // one calling thread's page-locked slot on one device
   char *h = nullptr;
   uint64_t d = 0;  // its device address
@@ -1970,7 +1980,10 @@ struct ZcSlot {  // one calling thread's page-locked slot on one device
   ZcSlot(const ZcSlot &) = delete;
   ZcSlot &operator=(const ZcSlot &) = delete;
   ~ZcSlot() {
-    if (h) (void)hipHostFree(h);
+    if (h) {
+      (void)hipHostFree(h);
+      g_zc_slot_bytes.fetch_sub(cap, std::memory_order_relaxed);
+    }
     if (flag && clean) {
       std::lock_guard<std::mutex> lk(g_signal_mu);
       signal_pool()[dev].push_back({flag, dflag, counter});
@@ -2722,16 +2735,28 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
   }
   const size_t need = static_cast<size_t>(nstripes) * nio * static_cast<size_t>(C);
   if (slot->cap < need) {
+    const size_t cap = std::max<size_t>(need, 256u << 10);
+    // all threads' slots together stay within LSEC_ZC_SLOTS_MB (default 1 GiB of page-locked
+    // memory); a call whose slot would pass it goes to the dispatcher's shared staging instead
+    if (g_zc_slot_bytes.load(std::memory_order_relaxed) - slot->cap + cap > zc_slot_budget()) return 1;
     if (slot->h) (void)hipHostFree(slot->h);
+    g_zc_slot_bytes.fetch_sub(slot->cap, std::memory_order_relaxed);
     slot->h = nullptr;
     slot->cap = 0;
-    const size_t cap = std::max<size_t>(need, 256u << 10);
+    slot->d = 0;
     // coherent: the kernel's reads and writes of the slot go straight over PCIe, none stays in an L2
-    HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&slot->h), cap, hipHostMallocCoherent));
+    char *h = nullptr;
     void *d = nullptr;
-    HIP_OK(hipHostGetDevicePointer(&d, slot->h, 0));
+    HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&h), cap, hipHostMallocCoherent));
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
+      (void)hipGetLastError();
+      (void)hipHostFree(h);
+      return fail("zero-copy slot: no device address");
+    }
+    slot->h = h;
     slot->d = reinterpret_cast<uint64_t>(d);
     slot->cap = cap;
+    g_zc_slot_bytes.fetch_add(cap, std::memory_order_relaxed);
   }
   ZcStats::get().launch_slot.fetch_add(1, std::memory_order_relaxed);
   // slot layout: inputs [s][nin][C], then outputs [s][nout][C]
@@ -2773,7 +2798,10 @@ bool zerocopy_enabled() {
 int run_host_auto(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
                   const std::vector<int> &out_ids, const void *image, int kind) {
   const size_t bytes = static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()) * C;
-  if (zerocopy_enabled() && bytes <= zerocopy_limit()) return run_zerocopy(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
+  if (zerocopy_enabled() && bytes <= zerocopy_limit()) {
+    const int rc = run_zerocopy(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
+    if (rc != 1) return rc;  // 1: its slot would pass the page-locked budget
+  }
   if (bytes <= coalesce_limit()) {
     static std::atomic<int> own_inflight{0};
     static const int own_max = [] {  // LSEC_OWN_PIPELINE_MAX: A/B runs (0: always the dispatcher)

@@ -109,15 +109,17 @@ REF = os.path.join(ROOT, "oracle", "_ref", "libjerasure_ref.so")
 
 
 @pytest.mark.skipif(not (os.path.exists(BENCH) and os.path.exists(REF)), reason="build/fnptr_bench or oracle/_ref not built")
-@pytest.mark.parametrize("chunk,threads,method,op,pinned", [
-    (16384, 128, "reed_sol_van", "encode", 0), (16384, 128, "cauchy_good", "decode", 0),
-    (65536, 64, "cauchy_good", "encode", 1), (1 << 20, 16, "reed_sol_van", "encode", 0)])
-def test_fn_pointer_stress_bit_exact(cuda, chunk, threads, method, op, pinned):
+@pytest.mark.parametrize("chunk,threads,method,op,pinned,extra", [
+    (16384, 128, "reed_sol_van", "encode", 0, {}), (16384, 128, "cauchy_good", "decode", 0, {}),
+    (65536, 64, "cauchy_good", "encode", 1, {}), (1 << 20, 16, "reed_sol_van", "encode", 0, {}),
+    (262144, 32, "reed_sol_van", "decode", 0, {"LSEC_ZC_SLOTS_MB": "4"})])
+def test_fn_pointer_stress_bit_exact(cuda, chunk, threads, method, op, pinned, extra):
     """LStore's pattern in C (tools/fnptr_bench.c, FNPTR_VERIFY=1): every thread calls
     encode_block / decode_block on its own stripe for 1 s; before each call the chunks it must
     write are overwritten, after it they must equal the reference's (oracle/_ref) -- every
-    call checked, at up to 128 threads (server slots, parking, one pointer query per call)."""
-    env = dict(os.environ, FNPTR_VERIFY="1", FNPTR_REF=REF, FNPTR_PINNED=str(pinned))
+    call checked, at up to 128 threads (server slots, parking, one pointer query per call; the
+    last case's zero-copy slots hit their page-locked budget and calls fall to the dispatcher)."""
+    env = dict(os.environ, FNPTR_VERIFY="1", FNPTR_REF=REF, FNPTR_PINNED=str(pinned), **extra)
     out = subprocess.run([BENCH, str(chunk), str(threads), "1", method, op], env=env, capture_output=True,
                          text=True, timeout=100)
     assert out.returncode == 0, (out.returncode, out.stdout[-500:], out.stderr[-500:])
