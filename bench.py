@@ -13,8 +13,13 @@ value = k*C*N*world / max_rank(step time) / 2^30  (data GiB/s, "N KiB stripes" =
 
 Launching.  `bench.py --gpus N` with WORLD_SIZE unset starts N ranks itself (spawned before
 anything touches the GPU); under torch.distributed.run (WORLD_SIZE set) it runs as one rank
-and refuses a WORLD_SIZE that disagrees with --gpus.  LSEC_DIST_BACKEND=gloo lets the ranks
-share one GPU (rehearsal); the default is RCCL ("nccl").
+and refuses a WORLD_SIZE that disagrees with --gpus.  The control plane (timing barrier, max,
+gather) runs over gloo: the data path needs no collective, and gloo also lets ranks share one
+GPU in a rehearsal.  LSEC_DIST_BACKEND=nccl puts it on RCCL instead.
+
+Placement.  Every rank pins itself to the CPUs of its GPU's NUMA node (lsec_device_numa: PCI bus
+id -> sysfs numa_node -> cpulist) before it allocates host buffers, so its host stripes, its
+staging and the engine threads it starts are node-local.
 
 Device-resident layout: data [N][k][C], parity [N][m][C] -- LStore's own layout (one cache
 page holds a stripe's k chunks back to back, cache.c:3843; the parity buffer holds m,
@@ -28,7 +33,9 @@ Also reported (same JSON line):
   cpu_baseline  the reference CPU path (oracle/_ref: vendor/jerasure via the plan dispatch)
                 on a bounded sample of the same workload, at 1 thread and at every usable
                 host core of this box
-  host_path     PCIe-inclusive rate of et_encode_stripes / et_decode_stripes from host memory
+  host_path     PCIe-inclusive rate of et_encode_stripes / et_decode_stripes from host memory;
+                at N > 1 every rank runs it at the same time (barrier before every timed pass):
+                per rank, and aggregated as sum of bytes / max time over ranks
   hbm_copy_ref  this box's device-to-device copy rate (the practical HBM ceiling) and the
                 encode / decode kernels' rates relative to it
 Every run checks parity bit-exactly against the reference (oracle/_ref) on sampled stripes.
@@ -229,12 +236,27 @@ def pmc_traffic_live(a, N):
             "launches": len(vals.get((name, "FETCH_SIZE"), []))}
 
 
-def host_path_rate(plan, k, m, C, lost, nstripes, pinned=False, reps=3):
+def host_path_aggregate(per_rank):
+    """N > 1: whole-node PCIe-inclusive rate from every rank's concurrent passes: for pass i,
+    sum of the ranks' user bytes / the slowest rank's time; median over passes."""
+    out = {}
+    for op in ("encode", "decode"):
+        reps = min(len(r["times"][op + "_s"]) for r in per_rank)
+        rates = sorted(sum(r["times"]["user_bytes"] for r in per_rank) /
+                       max(r["times"][op + "_s"][i] for r in per_rank) / 2**30 for i in range(reps))
+        out[op + "_gibps"] = round(rates[len(rates) // 2], 2)
+    out["combined_gibps"] = round(1 / (1 / out["encode_gibps"] + 1 / out["decode_gibps"]), 2)
+    return out
+
+
+def host_path_rate(plan, k, m, C, lost, nstripes, pinned=False, reps=3, barrier=None):
     """et_encode_stripes / et_decode_stripes from host memory (PCIe-inclusive), median of reps.
 
     pinned=False: pageable numpy buffers (LStore's cache pages) -> pinned in place or packed
     into the engine's pinned staging -> H2D -> kernel -> D2H.  pinned=True: page-locked buffers
-    (torch pin_memory = hipHostMalloc), DMA'd in place with no host copies."""
+    (torch pin_memory = hipHostMalloc), DMA'd in place with no host copies.  barrier: called
+    before every timed pass, so that ranks run their passes at the same time (N > 1); the raw
+    pass times are returned in "times" for the aggregate."""
     if pinned:
         import torch
         buf = torch.empty((nstripes, k + m, C), dtype=torch.uint8, pin_memory=True).numpy()
@@ -246,18 +268,23 @@ def host_path_rate(plan, k, m, C, lost, nstripes, pinned=False, reps=3):
     warm = min(nstripes, 16)  # a full staging batch: steady state, not first-call pinning
     plan.encode_stripes(buf[:warm])
     plan.decode_stripes(buf[:warm], [lost])
-    te, td = [], []
+    te_all, td_all = [], []
     for _ in range(reps):
+        if barrier:
+            barrier()
         t0 = time.perf_counter()
         plan.encode_stripes(buf)
-        te.append(time.perf_counter() - t0)
+        te_all.append(time.perf_counter() - t0)
+        if barrier:
+            barrier()
         t0 = time.perf_counter()
         plan.decode_stripes(buf, [lost])
-        td.append(time.perf_counter() - t0)
-    te, td = sorted(te)[reps // 2], sorted(td)[reps // 2]
+        td_all.append(time.perf_counter() - t0)
+    te, td = sorted(te_all)[reps // 2], sorted(td_all)[reps // 2]
     gib = k * C * nstripes / 2**30
     return {"encode_gibps": round(gib / te, 2), "decode_gibps": round(gib / td, 2),
             "combined_gibps": round(gib / (te + td), 2), "stripes": nstripes,
+            "times": {"encode_s": te_all, "decode_s": td_all, "user_bytes": k * C * nstripes},
             "note": ("page-locked host buffers -> DMA -> kernel -> DMA -> host" if pinned else
                      "pageable host buffers -> pinned staging -> H2D -> kernel -> D2H -> host")}
 
@@ -276,7 +303,18 @@ class HipEngine:
         self.torch, self.L, self.E, self.a = torch, L, E, a
         torch.cuda.set_device(local % torch.cuda.device_count())
         self.dev = torch.device("cuda", torch.cuda.current_device())
-        self.backend = os.environ.get("LSEC_DIST_BACKEND", "nccl") if world > 1 else None
+        # control plane only (barrier, max, gather): gloo by default, RCCL opt-in
+        self.backend = os.environ.get("LSEC_DIST_BACKEND", "gloo") if world > 1 else None
+        # this rank's host threads and host buffers on its GPU's NUMA node (lsec_device_numa)
+        self.numa = {"node": -1, "cpus": 0, "pinned": False}
+        try:
+            node, cpus = E.device_numa(self.dev.index)
+            self.numa.update(node=node, cpus=len(cpus))
+            if cpus and os.environ.get("LSEC_NUMA", "1") != "0":
+                os.sched_setaffinity(0, cpus)
+                self.numa["pinned"] = True
+        except (E.ErasureError, OSError) as ex:
+            self.numa["error"] = str(ex)
         bw_v, bs_v = (int(x) for x in a.variant.split(","))
         E.set_kernel_variant(bw_v, bs_v)
         self.method = E.JE_METHOD_NAMES.index(a.method)
@@ -376,9 +414,9 @@ class HipEngine:
         return ok, ("bit-exact vs oracle/_ref (vendor/jerasure) on stripes %s" % pick if ref else
                     "bit-exact vs the oracle restatement on stripes %s (_ref not built)" % pick)
 
-    def extras(self, N, t_enc, t_dec, rank, world):
-        """rank-0, N = 1 extras: the padded layout A/B, the HBM copy probe, the CPU reference
-        and the PCIe-inclusive host path."""
+    def extras(self, N, t_enc, t_dec, rank, world, barrier=None):
+        """N = 1 extras on rank 0: the padded layout A/B, the HBM copy probe and the CPU
+        reference.  The PCIe-inclusive host path runs on every rank (concurrently at N > 1)."""
         a, torch, lib, E = self.a, self.torch, self.lib, self.E
         k, m, C = a.k, a.m, a.chunk
         out = {}
@@ -468,11 +506,12 @@ class HipEngine:
         if rank == 0 and world == 1:
             # the reference CPU path is timed at N=1 only (at N>1 it would only delay the ranks' exit)
             out["cpu_baseline"] = None if a.no_cpu else cpu_baseline(self.method, k, m, C, self.P, a.lost, a.cpu_seconds)
-            if not a.no_host_path:
-                ns = max(8, min(256, (4 << 30) // ((k + m) * C)))
-                host = host_path_rate(self.plan, k, m, C, a.lost, ns)
-                host["pinned"] = host_path_rate(self.plan, k, m, C, a.lost, ns, pinned=True)
-                out["host_path"] = host
+        if not a.no_host_path:
+            # every rank: its own stripes from its own (node-local) host memory over its own link
+            ns = max(8, min(256, (4 << 30) // ((k + m) * C)))
+            host = host_path_rate(self.plan, k, m, C, a.lost, ns, barrier=barrier)
+            host["pinned"] = host_path_rate(self.plan, k, m, C, a.lost, ns, pinned=True, barrier=barrier)
+            out["host_path"] = host
         return out
 
     def kernel_name(self):
@@ -557,7 +596,23 @@ def run_rank(a, rank, world, local, engine_cls=HipEngine):
             print(json.dumps({"error": "parity mismatch vs reference", "per_rank": per_rank}), flush=True)
         raise SystemExit(1)
 
-    extras = eng.extras(N, t_enc, t_dec, rank, world)
+    extras = eng.extras(N, t_enc, t_dec, rank, world, barrier=dist.barrier if world > 1 else None)
+    host = extras.get("host_path")
+    if host is not None:
+        host["numa"] = getattr(eng, "numa", None)
+        if world > 1:
+            # every rank's concurrent host-path passes -> per-rank figures and the node aggregate
+            ranks = [None] * world
+            dist.all_gather_object(ranks, host)
+            agg = {"what": "all ranks at once: sum of user bytes / slowest rank's pass time, median of passes",
+                   "pageable": host_path_aggregate(ranks),
+                   "pinned": host_path_aggregate([r["pinned"] for r in ranks]),
+                   "per_rank": [{key: r.get(key) for key in ("encode_gibps", "decode_gibps", "numa")} |
+                                {"pinned": {key: r["pinned"][key] for key in ("encode_gibps", "decode_gibps")}}
+                                for r in ranks]}
+            host = dict(host, aggregate=agg)
+        host.pop("times", None)
+        host["pinned"].pop("times", None)
     if a.total_stripes > 0:
         value = k * C * a.total_stripes * a.steps / elapsed / 2**30
     else:
@@ -600,7 +655,7 @@ def run_rank(a, rank, world, local, engine_cls=HipEngine):
             "layout": extras.get("layout"),
             "hbm_copy_ref": extras.get("hbm_copy_ref"),
             "cpu_baseline": extras.get("cpu_baseline"),
-            "host_path": extras.get("host_path"),
+            "host_path": host,
             "parity_check": parity_note,
         }
         line = json.dumps(out)

@@ -218,6 +218,13 @@ int lsec_plan_jit(lio_erasure_plan_t *plan, const int *erasures);
  * smaller calls go to the listed devices in turn.  A device may be listed more than once.
  * 0 / -1 (unknown device). */
 int lsec_set_host_devices(const int *devices, int n);
+/* Host NUMA placement of device `dev`: its node (-1 if unknown) in *node and up
+ * to max_cpus of that node's CPUs this process may use in cpus[].  The engine pins a device's
+ * dispatcher thread, the threads running its share of a split host batch and the copy pool that
+ * packs its page-locked staging to these CPUs (LSEC_NUMA=0: no pinning).  A caller that owns a
+ * device (one process per GPU) can pin itself there before it allocates its host buffers.
+ * Returns the number of CPUs (0: no placement known), or -1 (no such device). */
+int lsec_device_numa(int dev, int *node, int *cpus, int max_cpus);
 
 /* Engine information / control */
 int lsec_abi_version(void);

@@ -14,6 +14,7 @@
 // abort() from the void encode_block fn-pointer).
 #include <hip/hip_runtime.h>
 #include <linux/futex.h>
+#include <pthread.h>
 #include <sched.h>
 #include <strings.h>
 #include <sys/syscall.h>
@@ -40,6 +41,7 @@
 #include "../../include/lstore_ec.h"
 #include "ec_host.h"
 #include "ec_jit.h"
+#include "ec_numa.h"
 #include "ec_kernels.h"
 #include "ec_server.h"
 #include "gf8.h"
@@ -708,11 +710,20 @@ struct CopyJob {
   size_t bytes;
 };
 
+// NUMA node whose copy pool packs this thread's staging: set by threads that work for one
+// device (its dispatcher, the threads of a split host batch), -1 elsewhere
+thread_local int tl_copy_node = -1;
+
 class CopyPool {
  public:
+  // one pool per NUMA node (workers pinned to the node's CPUs, ec_numa.h), plus an unpinned one
   static CopyPool &get() {
-    static CopyPool *pool = new CopyPool();  // intentionally leaked: workers live until exit
-    return *pool;
+    static std::mutex mu;
+    static auto *pools = new std::map<int, CopyPool *>();  // intentionally leaked: workers live until exit
+    std::lock_guard<std::mutex> lk(mu);
+    CopyPool *&p = (*pools)[tl_copy_node];
+    if (!p) p = new CopyPool(tl_copy_node);
+    return *p;
   }
 
   void run(std::vector<CopyJob> &jobs) {
@@ -752,12 +763,32 @@ class CopyPool {
     int users = 0;        // workers inside work() for this batch, guarded by mu_
   };
 
-  CopyPool() {
+  explicit CopyPool(int node) {
     const char *s = getenv("LSEC_COPY_THREADS");
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     const int n = s ? atoi(s) : static_cast<int>(std::min(8u, hw));
-    for (int i = 1; i < n; ++i) workers_.emplace_back([this] { loop(); });
+    std::vector<int> cpus;
+    if (node >= 0) cpus = node_cpus(node);
+    for (int i = 1; i < n; ++i)
+      workers_.emplace_back([this, cpus] {
+        if (!cpus.empty()) {
+          cpu_set_t set;
+          CPU_ZERO(&set);
+          for (int c : cpus) CPU_SET(c, &set);
+          (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+        }
+        loop();
+      });
     for (auto &t : workers_) t.detach();
+  }
+
+  // the CPUs of a node, from any device placed on it
+  static std::vector<int> node_cpus(int node) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) (void)hipGetLastError();
+    for (int d = 0; d < n; ++d)
+      if (lsec::numa::of_device(d).node == node) return lsec::numa::of_device(d).cpus;
+    return {};
   }
 
   // copies pieces until none are left; the caller of work() must hold a `users` reference
@@ -1849,6 +1880,10 @@ class Dispatcher {
   }
 
   void loop() {
+    // this device's host thread: on its NUMA node, packing with that node's copy pool, and
+    // allocating its page-locked staging from there
+    lsec::numa::bind_this_thread(dev_);
+    tl_copy_node = lsec::numa::of_device(dev_).node;
     if (hipSetDevice(dev_) != hipSuccess || hipStreamCreateWithFlags(&s_in_, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&s_out_, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&in_done_, hipEventDisableTiming) != hipSuccess ||
@@ -2382,6 +2417,11 @@ struct ZcStats {
 // call; the server's workgroups serve the parts of many callers in parallel.  The server exits
 // after 2 ms without work and is relaunched by the next caller (or by a waiting one that finds
 // it gone).  LSEC_SERVER=0 turns it off.
+// the stripe server's answer time limit (LSEC test hook lsec_test_server_hold) and its hold
+std::atomic<int> g_srv_timeout_ms{5000};
+std::atomic<int> g_srv_hold{0};
+std::atomic<unsigned long long> g_st_srv_timeouts{0};
+
 class StripeServer {
  public:
   static StripeServer *for_device(int dev) {
@@ -2417,6 +2457,13 @@ class StripeServer {
     };
     if (nin < 1 || nout < 1 || nin > lsec::kSrvMaxK || nout > lsec::kSrvMaxR) return refuse();
     if (kind != KBYTEWISE && kind != KBITSLICED) return refuse();
+    // a server that cannot be set up or launched is never posted to: the call takes its own
+    // zero-copy launch or the dispatcher (a post nobody will serve would strand its slots)
+    if (broken_.load(std::memory_order_acquire)) return refuse();
+    if (init_once()) {
+      broken_ = true;
+      return refuse();
+    }
     const lio_erasure_plan_t *p = &e->pub;
     const bool direct = cp && cp->by_kernel;
     // parts: column blocks of about 4 KiB per shard (one 256-lane x 16 B pass), whole
@@ -2458,10 +2505,6 @@ class StripeServer {
         return 1;
       }
     }
-    if (init_once()) {
-      release(nparts, slot);
-      return -1;
-    }
     uint32_t want[kMaxParts];
     for (int q = 0; q < nparts; ++q) {
       const int sl = slot[q];
@@ -2496,6 +2539,8 @@ class StripeServer {
     auto last_check = t0;
     const unsigned *flags[kMaxParts];
     for (int q = 0; q < nparts; ++q) flags[q] = &sh_->done[slot[q]][0];
+    const auto timeout = std::chrono::milliseconds(g_srv_timeout_ms.load(std::memory_order_relaxed));
+    bool late = false;
     // spin or park (FlagWaits) until every part is done, checking every 500 us that the server
     // has not retired meanwhile (it retires only after 2 ms without work; at 100 us slices a
     // loaded box woke 1.5 parked waiters per call just to check, profiles/r02_v30_zc_phases3.txt)
@@ -2505,11 +2550,23 @@ class StripeServer {
         last_check = now;
         if ((rc = ensure_running(true))) break;
       }
-      if (now - t0 > std::chrono::seconds(5)) {
-        rc = fail("stripe server: no answer for 5 s");
-        broken_ = true;
+      if (now - t0 > timeout) {
+        late = true;
         break;
       }
+    }
+    if (rc != 0 || late) {
+      // No answer in time (a throttled box, a stuck server) or no server: stop it and wait until
+      // it has left, so no post of this call can be served after the call returns -- for
+      // page-locked callers the server writes the caller's own buffers.  Parts served meanwhile
+      // count; the others are cancelled and the call takes another route (return 1).
+      g_st_srv_timeouts.fetch_add(1, std::memory_order_relaxed);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (stop_and_settle(nparts, slot, want) != nparts) {
+        release(nparts, slot);
+        return 1;
+      }
+      rc = 0;
     }
     const auto t_waited = std::chrono::steady_clock::now();
     if (stats) c_waited = thread_cpu_ns();
@@ -2531,7 +2588,7 @@ class StripeServer {
         const char *region = data_ + static_cast<size_t>(slot[q]) * kSlotBytes;
         for (size_t r = 0; r < nout; ++r) std::memcpy(ptrs[out_ids[r]] + c0, region + (nin + r) * n, static_cast<size_t>(n));
       }
-    if (rc == 0) release(nparts, slot);  // a slot whose post may still be served is never handed out again
+    release(nparts, slot);
     if (rc == 0 && stats) {
       ZcStats &z = ZcStats::get();
       const auto ns = [](std::chrono::steady_clock::duration d) {
@@ -2572,11 +2629,48 @@ class StripeServer {
   static void stop_all() {
     for (StripeServer *s : registry()) {
       std::lock_guard<std::mutex> lk(s->mu_);
-      if (!s->sh_ || !s->running_) continue;
-      for (int g = 0; g < lsec::kSrvWG; ++g) __atomic_store_n(&s->sh_->post[g][lsec::kSrvSlotsPerWG], 1u, __ATOMIC_RELEASE);
-      (void)hipEventSynchronize(s->ev_);
-      s->running_ = false;
+      if (s->sh_) s->stop_and_settle(0, nullptr, nullptr);
     }
+  }
+
+ public:
+  // test hook (lsec_test_server_hold): stop every server, so the next launch takes the new hold
+  static void restart_all() { stop_all(); }
+
+ private:
+  // Stop the running server and wait (bounded) until it has left.  The stop word makes it serve
+  // what is posted and exit; afterwards nothing can serve a post until the next launch, which
+  // takes served[] from done[].  Of this call's parts, those served count; the rest are
+  // cancelled by setting done to the posted value, so no later launch serves them.  Returns
+  // the number served.  mu_ held.  A server that never leaves ends the process: a caller's
+  // page-locked buffers may not be handed back while a kernel can still write them.
+  int stop_and_settle(int nparts, const int *slot, const uint32_t *want) {
+    if (running_) {
+      for (int g = 0; g < lsec::kSrvWG; ++g) __atomic_store_n(&sh_->post[g][lsec::kSrvSlotsPerWG], 1u, __ATOMIC_RELEASE);
+      const auto t0 = std::chrono::steady_clock::now();
+      for (;;) {
+        const hipError_t q = hipEventQuery(ev_);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) {  // the device failed: nothing runs there any more
+          (void)hipGetLastError();
+          broken_ = true;
+          break;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+          fprintf(stderr, "liblstore_ec: the stripe server on device %d did not stop within 30 s; aborting\n", dev_);
+          abort();
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+      }
+      running_ = false;
+    }
+    int served = 0;
+    for (int q = 0; q < nparts; ++q) {
+      unsigned *d = &sh_->done[slot[q]][0];
+      if (__atomic_load_n(d, __ATOMIC_ACQUIRE) == want[q]) ++served;
+      else __atomic_store_n(d, want[q], __ATOMIC_RELEASE);
+    }
+    return served;
   }
 
   bool claim(int n, int *slot) {
@@ -2616,7 +2710,18 @@ class StripeServer {
     void *p = nullptr;
     HIP_OK(hipHostGetDevicePointer(&p, sh_, 0));
     sh_dev_ = reinterpret_cast<uint64_t>(p);
-    HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&data_), kSlotBytes * lsec::kSrvSlots, hipHostMallocCoherent));
+    // the slot region counts against the zero-copy page-locked budget (LSEC_ZC_SLOTS_MB) like
+    // the threads' own slots: about 93 MiB per device
+    const size_t region = kSlotBytes * lsec::kSrvSlots;
+    if (g_zc_slot_bytes.fetch_add(region, std::memory_order_relaxed) + region > zc_slot_budget()) {
+      g_zc_slot_bytes.fetch_sub(region, std::memory_order_relaxed);
+      return fail("stripe server: its %zu MiB of slots would pass the page-locked budget (LSEC_ZC_SLOTS_MB)", region >> 20);
+    }
+    if (hipHostMalloc(reinterpret_cast<void **>(&data_), region, hipHostMallocCoherent) != hipSuccess) {
+      (void)hipGetLastError();
+      g_zc_slot_bytes.fetch_sub(region, std::memory_order_relaxed);
+      return fail("stripe server: cannot allocate its slots");
+    }
     HIP_OK(hipHostGetDevicePointer(&p, data_, 0));
     data_dev_ = reinterpret_cast<uint64_t>(p);
     ready_.store(true, std::memory_order_release);
@@ -2642,7 +2747,10 @@ class StripeServer {
     if (running_ && check) {
       const hipError_t q = hipEventQuery(ev_);
       if (q == hipSuccess) running_ = false;
-      else if (q != hipErrorNotReady) return fail("stripe server: %s", hipGetErrorString(q));
+      else if (q != hipErrorNotReady) {
+        broken_ = true;
+        return fail("stripe server: %s", hipGetErrorString(q));
+      }
     }
     if (running_) return 0;
     for (int g = 0; g < lsec::kSrvWG; ++g) sh_->post[g][lsec::kSrvSlotsPerWG] = 0;  // stop word
@@ -2650,11 +2758,16 @@ class StripeServer {
     a.shared = reinterpret_cast<lsec::SrvShared *>(sh_dev_);
     a.votes = votes_;
     a.idle_ticks = 200000;  // 2 ms at the 100 MHz wall clock
+    a.hold = g_srv_hold.load(std::memory_order_relaxed) ? 1u : 0u;
+    a.pad = 0;
     DeviceGuardLite g(dev_);
     hipError_t err = hipMemsetAsync(votes_, 0, sizeof(int), st_);
     if (err == hipSuccess) err = lsec::launch_stripe_server(a, st_);
     if (err == hipSuccess) err = hipEventRecord(ev_, st_);
-    if (err != hipSuccess) return fail("stripe server launch: %s", hipGetErrorString(err));
+    if (err != hipSuccess) {
+      broken_ = true;
+      return fail("stripe server launch: %s", hipGetErrorString(err));
+    }
     running_ = true;
     return 0;
   }
@@ -2922,11 +3035,19 @@ int on_host_devices(int nstripes, size_t bytes, F &&fn) {
     const int base = nstripes / G, extra = nstripes % G;
     const int s0 = g * base + std::min(g, extra), n = base + (g < extra ? 1 : 0);
     DeviceGuard dg(devs[g]);
+    // each range packs with its device's node-local copy pool (ec_numa.h)
+    const int node0 = tl_copy_node;
+    tl_copy_node = lsec::numa::of_device(devs[g]).node;
     rc[g] = dg.ok ? fn(s0, n) : fail("cannot select device %d", devs[g]);
+    tl_copy_node = node0;
     if (rc[g]) err[g] = tl_err;  // tl_err is per thread
   };
   std::vector<std::thread> th;
-  for (int g = 1; g < G; ++g) th.emplace_back(work, g);
+  for (int g = 1; g < G; ++g)
+    th.emplace_back([&work, &devs, g] {
+      lsec::numa::bind_this_thread(devs[g]);  // a range thread of its own: on its device's node
+      work(g);
+    });
   work(0);
   for (auto &t : th) t.join();
   for (int g = 0; g < G; ++g)
@@ -3870,6 +3991,40 @@ int lsec_hbm_mix_dev(const lsec_shard_t *shards, int k, int m, int nstripes, lon
 // sets its 1..16 flags in random order after a random delay of 0-300 us, `iters` rounds.  Every
 // wait must end with all its flags set and within 2 s.  Test hook, not part of include/*.h;
 // needs no GPU.  Returns 0, or -1 with a message.
+// Test hook, not part of include/*.h: hold = 1 makes stripe servers launched from now on poll
+// but serve nothing (a server that never answers); timeout_ms sets how long a call waits for
+// its parts (default 5000).  Running servers are stopped so the next launch takes the setting.
+// Returns the number of server calls that have timed out (or lost their server) so far.
+int lsec_device_numa(int dev, int *node, int *cpus, int max_cpus) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    n = 0;
+  }
+  if (dev < 0 || dev >= n) return fail("lsec_device_numa: no device %d", dev);
+  const lsec::numa::Placement &pl = lsec::numa::of_device(dev);
+  if (node) *node = pl.node;
+  for (int i = 0; cpus && i < max_cpus && i < static_cast<int>(pl.cpus.size()); ++i) cpus[i] = pl.cpus[i];
+  return static_cast<int>(pl.cpus.size());
+}
+
+// Test hook, not part of include/*.h: the placement of PCI function `bus` under the sysfs tree
+// `root` (a fake tree in tests/test_numa.py), unfiltered by this process's affinity.
+int lsec_test_numa_for_bus(const char *root, const char *bus, int *node, int *cpus, int max_cpus) {
+  if (!root || !bus) return fail("lsec_test_numa_for_bus: NULL argument");
+  const lsec::numa::Placement pl = lsec::numa::for_bus(root, bus, {});
+  if (node) *node = pl.node;
+  for (int i = 0; cpus && i < max_cpus && i < static_cast<int>(pl.cpus.size()); ++i) cpus[i] = pl.cpus[i];
+  return static_cast<int>(pl.cpus.size());
+}
+
+long long lsec_test_server_hold(int hold, int timeout_ms) {
+  if (hold >= 0) g_srv_hold.store(hold ? 1 : 0);
+  if (timeout_ms > 0) g_srv_timeout_ms.store(timeout_ms);
+  if (hold >= 0) StripeServer::restart_all();
+  return static_cast<long long>(g_st_srv_timeouts.load());
+}
+
 int lsec_selftest_waits(int threads, int iters) {
   if (threads < 1 || threads > 512 || iters < 1) return fail("lsec_selftest_waits: bad arguments");
   struct alignas(64) Pair {

@@ -276,17 +276,20 @@ struct Entry {
   std::string err;
 };
 
-std::mutex g_mu;
-std::condition_variable g_cv;
+// leaked on purpose: a compile thread still running when the process exits may touch them
+std::mutex &g_mu = *new std::mutex();
+std::condition_variable &g_cv = *new std::condition_variable();
 int g_compiling = 0;  // compile threads still running (waited for at exit, below)
+// bumped whenever an image is bound or unbound: invalidates the threads' ready() caches
+std::atomic<uint64_t> g_gen{1};
 
-// at exit: let running compiles finish (bounded) before the statics they use are destroyed
+// at exit: give running compiles a short while to finish (they touch only leaked state)
 void drain_compiles() {
   std::unique_lock<std::mutex> lk(g_mu);
-  g_cv.wait_for(lk, std::chrono::seconds(60), [] { return g_compiling == 0; });
+  g_cv.wait_for(lk, std::chrono::seconds(2), [] { return g_compiling == 0; });
 }
-std::map<std::vector<uint8_t>, std::shared_ptr<Entry>> g_by_matrix;  // key: R, K, matrix
-std::map<const void *, std::shared_ptr<Entry>> g_by_image;           // device image -> entry
+auto &g_by_matrix = *new std::map<std::vector<uint8_t>, std::shared_ptr<Entry>>();  // key: R, K, matrix
+auto &g_by_image = *new std::map<const void *, std::shared_ptr<Entry>>();           // device image -> entry
 
 std::vector<uint8_t> key_of(const uint8_t *mat, int R, int K) {
   std::vector<uint8_t> k(2 + static_cast<size_t>(R) * K);
@@ -372,6 +375,7 @@ void bind(const void *image, const uint8_t *mat, int R, int K) {
       e = it->second;
     }
     g_by_image[image] = e;
+    g_gen.fetch_add(1, std::memory_order_acq_rel);
   }
   if (start) std::thread(compile, e).detach();
 }
@@ -379,6 +383,7 @@ void bind(const void *image, const uint8_t *mat, int R, int K) {
 void unbind(const void *image) {
   std::lock_guard<std::mutex> lk(g_mu);
   g_by_image.erase(image);
+  g_gen.fetch_add(1, std::memory_order_acq_rel);
 }
 
 int wait(const void *image, int timeout_ms) {
@@ -391,12 +396,33 @@ int wait(const void *image, int timeout_ms) {
 }
 
 hipFunction_t ready(const void *image, int R, int K) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  // per-thread cache of ready kernels: per-stripe launches from hundreds of pool threads take no
+  // lock once their network is loaded (a bind or unbind anywhere empties every cache)
+  struct Key {
+    const void *image;
+    int dev, R, K;
+    bool operator<(const Key &o) const {
+      return image != o.image ? image < o.image : dev != o.dev ? dev < o.dev : R != o.R ? R < o.R : K < o.K;
+    }
+  };
+  thread_local std::map<Key, hipFunction_t> cache;
+  thread_local uint64_t cache_gen = 0;
+  const uint64_t gen = g_gen.load(std::memory_order_acquire);
+  if (cache_gen != gen) {
+    cache.clear();
+    cache_gen = gen;
+  }
+  const Key key{image, dev, R, K};
+  auto c = cache.find(key);
+  if (c != cache.end()) return c->second;
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_by_image.find(image);
   if (it == g_by_image.end() || it->second->R != R || it->second->K != K) return nullptr;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  return function_locked(*it->second, dev);
+  hipFunction_t fn = function_locked(*it->second, dev);
+  if (fn && g_gen.load(std::memory_order_acquire) == gen) cache[key] = fn;  // not yet ready: ask again next time
+  return fn;
 }
 
 hipError_t launch(hipFunction_t fn, int R, int K, const ShardRef *in, const ShardRef *out, int nstripes, int64_t size,

@@ -46,6 +46,8 @@ struct SrvArgs {
   SrvShared *shared;   // device address of the shared block
   int *votes;          // device memory: workgroups that voted to retire (zeroed before a launch)
   uint64_t idle_ticks; // 100 MHz wall clock ticks of idleness before a workgroup votes
+  uint32_t hold;       // test hook: nonzero = poll but serve nothing (lsec_test_server_hold)
+  uint32_t pad;
 };
 
 hipError_t launch_stripe_server(const SrvArgs &a, hipStream_t stream);

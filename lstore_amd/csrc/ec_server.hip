@@ -164,26 +164,39 @@ __global__ __launch_bounds__(kBlock) void k_stripe_server(SrvArgs a) {
     if (threadIdx.x < 64) {  // wave 0 polls this workgroup's line
       const int lane = threadIdx.x;
       const uint32_t v = lane < 32 ? sys_load(&sh->post[g][lane]) : 0u;
-      const bool ready = lane < kSrvSlotsPerWG && v != served[lane];
+      // a.hold (test hook, lsec_test_server_hold): serve nothing, as a server that never answers
+      const bool ready = lane < kSrvSlotsPerWG && v != served[lane] && !a.hold;
       const uint64_t m = __ballot(ready);
       const uint32_t stop = __shfl(v, kSrvSlotsPerWG);
       // round robin: the first ready slot after the last one served, so slots that other
       // threads keep re-posting cannot starve a higher one
       const uint64_t after = m & ~((2ull << last_pick) - 1);
       const uint64_t pool = after ? after : m;
-      const int first = pool ? __ffsll(static_cast<unsigned long long>(pool)) - 1 : -1;
+      int first = pool ? __ffsll(static_cast<unsigned long long>(pool)) - 1 : -1;
       const uint32_t val = __shfl(v, first < 0 ? 0 : first);
       if (lane == 0) {
-        pick = first;
-        pick_val = val;
         int q = stop != 0;
-        if (first >= 0) {
-          last_pick = first;
-          if (voted) {  // work again: take back the idle vote before serving
-            __hip_atomic_fetch_add(a.votes, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (first >= 0 && voted) {
+          // work again: take back the idle vote before serving -- unless the count is complete.
+          // Retirement is a one-way latch: once every workgroup has voted, a workgroup that has
+          // seen the full count may already have left (stranding its slots), so nobody may take
+          // a vote back; this one leaves too and the post waits for the next launch, which
+          // reloads served[] from done[] (a compare-and-swap refuses at kSrvWG).
+          int cur = __hip_atomic_fetch_add(a.votes, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          while (cur < kSrvWG &&
+                 !__hip_atomic_compare_exchange_strong(a.votes, &cur, cur - 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)) {
+          }
+          if (cur >= kSrvWG) {
+            first = -1;
+            q = 1;
+          } else {
             voted = 0;
           }
-        } else {
+        }
+        if (first >= 0) {
+          last_pick = first;
+        } else if (!q) {
           // Exit is collective: a workgroup that left on its own would strand its slots while
           // the rest keep the kernel (and so the host's relaunch) waiting.  Idle workgroups
           // vote; all leave once every one has voted.  The count is read by an atomic
@@ -195,6 +208,8 @@ __global__ __launch_bounds__(kBlock) void k_stripe_server(SrvArgs a) {
           }
           if (voted && __hip_atomic_fetch_add(a.votes, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= kSrvWG) q = 1;
         }
+        pick = first;
+        pick_val = val;
         quit = q;
       }
     }

@@ -78,7 +78,7 @@ EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan",
            "lsec_decode_dev", "et_encode_stripes_magic", "et_stripes_magic", "lsec_encode_magic_dev",
            "lsec_stripe_magic_dev", "lsec_segment_write", "lsec_segment_write_iov", "lsec_segment_read", "lsec_segment_inspect",
            "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count", "lsec_last_error", "lsec_plan_kernel",
-           "lsec_set_kernel_variant", "lsec_set_host_devices", "lsec_hbm_copy_dev", "lsec_hbm_mix_dev", "lsec_prepare_encode", "lsec_plan_jit")
+           "lsec_set_kernel_variant", "lsec_set_host_devices", "lsec_hbm_copy_dev", "lsec_hbm_mix_dev", "lsec_prepare_encode", "lsec_plan_jit", "lsec_device_numa")
 
 # read / inspect flags and stripe states (include/lstore_ec.h)
 READ_PARANOID, MAGIC_LEGACY, INSPECT_FIX, MAX_DEVS = 1, 2, 4, 256
@@ -151,6 +151,10 @@ def lib():
     L.lsec_set_host_devices.argtypes = [C.POINTER(C.c_int), C.c_int]
     L.lsec_hbm_copy_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_ulonglong, C.c_void_p]
     L.lsec_hbm_mix_dev.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_void_p]
+    L.lsec_device_numa.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int]
+    L.lsec_test_numa_for_bus.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int]
+    L.lsec_test_server_hold.restype = C.c_longlong
+    L.lsec_test_server_hold.argtypes = [C.c_int, C.c_int]
     _lib = L
     return L
 
@@ -475,6 +479,26 @@ def set_host_devices(devices: Sequence[int] = ()) -> None:
     """lsec_set_host_devices: devices serving host-memory calls (empty = the current device)."""
     arr = (C.c_int * max(1, len(devices)))(*devices)
     _check(lib().lsec_set_host_devices(arr, len(devices)), "lsec_set_host_devices")
+
+
+def device_numa(dev: int) -> tuple[int, list[int]]:
+    """lsec_device_numa: (NUMA node or -1, the node's CPUs this process may use) of device dev."""
+    node = C.c_int(-1)
+    cpus = (C.c_int * 4096)()
+    n = lib().lsec_device_numa(dev, C.byref(node), cpus, 4096)
+    if n < 0:
+        raise ErasureError(f"lsec_device_numa failed: {last_error()}")
+    return node.value, list(cpus[:n])
+
+
+def numa_for_bus(root: str, bus: str) -> tuple[int, list[int]]:
+    """Test hook: the placement of PCI function `bus` under the sysfs tree `root`."""
+    node = C.c_int(-1)
+    cpus = (C.c_int * 4096)()
+    n = lib().lsec_test_numa_for_bus(root.encode(), bus.encode(), C.byref(node), cpus, 4096)
+    if n < 0:
+        raise ErasureError(f"lsec_test_numa_for_bus failed: {last_error()}")
+    return node.value, list(cpus[:n])
 
 
 def set_kernel_variant(bytewise: int = 0, bitsliced: int = 0) -> None:

@@ -19,6 +19,22 @@ import bench
 from lstore_amd.partition import stripe_range
 
 
+class _OracleHostPlan:
+    """Plan.encode_stripes / decode_stripes over the CPU oracle (test infrastructure only)."""
+
+    def __init__(self, O, method, k, m, P):
+        self.O, self.method, self.k, self.m, self.P = O, method, k, m, P
+        self.barriers = 0
+
+    def encode_stripes(self, buf):
+        for s in range(buf.shape[0]):
+            buf[s, self.k:] = self.O.encode(self.method, buf[s, :self.k], self.m, self.P)
+
+    def decode_stripes(self, buf, lost):
+        for s in range(buf.shape[0]):
+            assert self.O.decode(self.method, buf[s], self.k, list(lost), self.P) == 0
+
+
 class OracleEngine:
     """bench.HipEngine's interface over the CPU oracle (test infrastructure only)."""
 
@@ -79,8 +95,15 @@ class OracleEngine:
                 json.dump(crcs, f)
         return ok, "rebuilt == lost shard (oracle engine)"
 
-    def extras(self, N, t_enc, t_dec, rank, world):
-        return {}
+    def extras(self, N, t_enc, t_dec, rank, world, barrier=None):
+        if self.a.no_host_path:
+            return {}
+        # bench.host_path_rate's concurrent passes over the oracle (both legs pageable here: no
+        # page-locked memory without a GPU)
+        plan = _OracleHostPlan(self.O, self.method, self.a.k, self.a.m, self.P)
+        host = bench.host_path_rate(plan, self.a.k, self.a.m, self.a.chunk, self.a.lost, 4, barrier=barrier)
+        host["pinned"] = bench.host_path_rate(plan, self.a.k, self.a.m, self.a.chunk, self.a.lost, 4, barrier=barrier)
+        return {"host_path": host}
 
     def kernel_name(self):
         return "oracle (test engine)"
@@ -138,6 +161,34 @@ def test_self_launched_weak_scaling(built, tmp_path, monkeypatch):
     for r in range(2):
         seen |= {int(s) for s in json.loads((tmp_path / f"rank{r}.json").read_text())}
     assert seen == set(range(6))  # rank r owns stripes [3r, 3r+3)
+
+
+def test_host_path_on_every_rank_with_aggregate(built, tmp_path, monkeypatch):
+    """N > 1: every rank times the host path (its passes barrier-aligned with the other ranks'),
+    and rank 0 reports per-rank rates and the aggregate (sum of bytes / slowest rank's time)."""
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    out = tmp_path / "line.json"
+    args = bench.parse(["--chunk", "4096", "--steps", "1", "--warmup", "0", "--no-cpu", "--no-layout-ab",
+                        "--no-copy-ref", "--gpus", "2", "--stripes", "2", "--json-out", str(out)])
+    assert bench.launch(args, OracleEngine) == 0
+    line = json.loads(out.read_text())
+    host = line["host_path"]
+    agg = host["aggregate"]
+    assert len(agg["per_rank"]) == 2
+    for leg in ("pageable", "pinned"):
+        assert agg[leg]["encode_gibps"] > 0 and agg[leg]["decode_gibps"] > 0
+    # the aggregate is at most the sum of the ranks' own (median) rates, at least the slowest rank's
+    assert agg["pageable"]["encode_gibps"] >= 0.5 * min(r["encode_gibps"] for r in agg["per_rank"])
+    assert "times" not in host and "times" not in host["pinned"]
+
+
+def test_host_path_aggregate_is_sum_over_max():
+    ranks = [{"times": {"encode_s": [1.0, 2.0, 1.0], "decode_s": [1.0, 1.0, 1.0], "user_bytes": 2**30}},
+             {"times": {"encode_s": [2.0, 1.0, 4.0], "decode_s": [0.5, 0.5, 0.5], "user_bytes": 2**30}}]
+    agg = bench.host_path_aggregate(ranks)
+    assert agg["encode_gibps"] == 1.0  # passes: 2/2, 2/2, 2/4 -> median 1
+    assert agg["decode_gibps"] == 2.0
+    assert agg["combined_gibps"] == round(1 / (1 / 1.0 + 1 / 2.0), 2)
 
 
 def test_world_size_must_match_gpus(built, monkeypatch, capsys):

@@ -103,6 +103,51 @@ def test_new_plans_while_the_server_runs(cuda):
             assert np.array_equal(sh[k:], O.encode(method, np.ascontiguousarray(sh[:k]), m, p.packet_size)), round_
 
 
+def test_server_timeout_leaves_no_late_writes(cuda):
+    """A call whose parts the stripe server does not answer in time (the test hook holds every
+    post) stops the server, cancels its parts and takes its own launch.  Nothing may serve those
+    parts after the call has returned: the caller's page-locked chunks are served in place, so a
+    late serve would write stale parity into buffers the caller has already reused."""
+    import ctypes as C
+
+    lib = L.lib()
+    lib.lsec_test_server_hold.restype = C.c_longlong
+    lib.lsec_test_server_hold.argtypes = [C.c_int, C.c_int]
+    method, k, m, C_ = L.REED_SOL_VAN, 6, 3, 16384
+    rng = np.random.default_rng(77)
+    with L.Plan.for_chunk(method, k, m, C_) as p:
+        t0 = lib.lsec_test_server_hold(1, 200)
+        try:
+            held = [_pinned((k + m, C_)), np.empty((k + m, C_), np.uint8)]
+            for sh in held:
+                sh[:k] = rng.integers(0, 256, (k, C_), dtype=np.uint8)
+                sh[k:] = 0
+                start = time.perf_counter()
+                p.encode_block([sh[i] for i in range(k + m)])
+                assert time.perf_counter() - start >= 0.15  # it waited for the held server
+                assert np.array_equal(sh[k:], O.encode(method, np.ascontiguousarray(sh[:k]), m, p.packet_size))
+                full = sh.copy()
+                sh[1] = 0xEE
+                assert p.decode_block([sh[i] for i in range(k + m)], [1]) == 0
+                assert np.array_equal(sh, full)
+            assert lib.lsec_test_server_hold(-1, 0) - t0 >= 4  # every call above timed out
+        finally:
+            lib.lsec_test_server_hold(0, 5000)
+        # the caller reuses its buffers; the server now serves again (other calls relaunch it)
+        for sh in held:
+            sh[:] = 0xA5
+        snap = [sh.copy() for sh in held]
+        other = np.empty((k + m, C_), np.uint8)
+        for it in range(20):
+            other[:k] = rng.integers(0, 256, (k, C_), dtype=np.uint8)
+            p.encode_block([other[i] for i in range(k + m)])
+            assert np.array_equal(other[k:], O.encode(method, np.ascontiguousarray(other[:k]), m, p.packet_size))
+            time.sleep(0.001 if it % 5 else 0.005)  # across idle retirements and relaunches
+        time.sleep(0.05)
+        for sh, want in zip(held, snap):
+            assert np.array_equal(sh, want), "a cancelled part was served after its call returned"
+
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BENCH = os.path.join(ROOT, "build", "fnptr_bench")
 REF = os.path.join(ROOT, "oracle", "_ref", "libjerasure_ref.so")
