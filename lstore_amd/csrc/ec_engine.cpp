@@ -3963,6 +3963,10 @@ void lsec_set_kernel_variant(int bytewise_variant, int bitsliced_variant) {
   lsec::set_kernel_variant(bytewise_variant, bitsliced_variant);
 }
 
+// Tuning hook, not part of include/*.h: force the tile order of the bytewise and bit-sliced
+// kernels (ApplyArgs::order; -1 restores the default policy).
+void lsec_set_tile_order(int order) { lsec::set_tile_order(order); }
+
 int lsec_hbm_copy_dev(void *dst, const void *src, unsigned long long bytes, void *stream) {
   const hipError_t e = lsec::launch_hbm_copy(dst, src, bytes, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return fail("lsec_hbm_copy_dev: %s", hipGetErrorString(e));

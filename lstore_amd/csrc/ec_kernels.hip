@@ -10,6 +10,13 @@ namespace lsec {
 namespace {
 
 int g_bw_variant = 0, g_bs_variant = 0;
+int g_tile_order = -1;  // -1: the default policy (tile_order below); else forced (lsec_set_tile_order)
+
+// Tile order of the bytewise and bitsliced kernels (ApplyArgs::order, tile_at).
+int tile_order(const ApplyArgs &a) {
+  if (g_tile_order >= 0) return g_tile_order;
+  return 0;
+}
 
 int default_grid(uint64_t ntiles) {
   // One tile per block: on this streaming pattern a full grid beat every grid-stride
@@ -57,6 +64,8 @@ void set_kernel_variant(int bw, int bs) {
   g_bs_variant = bs;
 }
 
+void set_tile_order(int order) { g_tile_order = order; }
+
 int bytewise_variant() { return g_bw_variant; }
 
 hipError_t launch_bytewise(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
@@ -67,7 +76,9 @@ hipError_t launch_bytewise(const ApplyArgs &a, hipStream_t st, int grid_blocks) 
   const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);
-  return by_r(a.R, [&](auto r) { return dispatch_bytewise<decltype(r)::value>(a, st, grid, shape); });
+  ApplyArgs b = a;
+  b.order = tile_order(a);
+  return by_r(a.R, [&](auto r) { return dispatch_bytewise<decltype(r)::value>(b, st, grid, shape); });
 }
 
 hipError_t launch_bytewise_magic(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
@@ -77,7 +88,9 @@ hipError_t launch_bytewise_magic(const ApplyArgs &a, hipStream_t st, int grid_bl
   const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);
-  return by_r(a.R, [&](auto r) { return dispatch_bytewise_magic<decltype(r)::value>(a, st, grid); });
+  ApplyArgs b = a;
+  b.order = tile_order(a);
+  return by_r(a.R, [&](auto r) { return dispatch_bytewise_magic<decltype(r)::value>(b, st, grid); });
 }
 
 hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
@@ -92,7 +105,9 @@ hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid_blocks)
   const uint64_t ntiles = ((col_bytes + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);
-  return by_r(a.R, [&](auto r) { return dispatch_bitsliced<decltype(r)::value>(a, st, grid, dw); });
+  ApplyArgs b = a;
+  b.order = tile_order(a);
+  return by_r(a.R, [&](auto r) { return dispatch_bitsliced<decltype(r)::value>(b, st, grid, dw); });
 }
 
 bool bitmatrix_w_supported(int w) {
