@@ -85,6 +85,7 @@ struct DecodeEntry {
   std::map<int, CoefCell *> dev_cells;  // device -> e x k cells
   std::vector<uint32_t> masks;          // bitmatrix codes: (e*w) x k row masks; wordwise: e x k x w products
   std::map<int, uint32_t *> dev_masks;
+  std::vector<uint32_t> wrows;          // wordwise: the e x k GF(2^w) decode rows (XOR networks)
 };
 
 constexpr int kFastDevs = 16;  // devices whose encode image pointer is cached lock-free
@@ -426,6 +427,8 @@ int encode_cells_locked(PlanExt *e, int dev, const void **out) {
       uint32_t *d = nullptr;
       if (upload_masks(e->impl->enc_masks, &d)) return -1;
       it = e->impl->enc_dev_masks.emplace(dev, d).first;
+      if (kernel_kind(e->pub.method, e->pub.w) == KWORDWISE)  // RS / r6 at w = 16 / 32: a bit-sliced network
+        lsec::jit::bind_w(d, e->impl->coding_w.data(), encode_rows(e), e->pub.data_strips, e->pub.w);
     }
     *out = it->second;
     return 0;
@@ -525,6 +528,7 @@ int decode_entry_locked(PlanExt *e, const std::vector<int> &ids, int dev, Decode
       group_image(ent.masks, static_cast<int>(wp.erased.size()), k, w);
       ent.xor_only = std::all_of(wp.rows.begin(), wp.rows.end(), [](uint32_t c) { return c <= 1u; });
       if (ent.xor_only) ent.dp.rows.assign(wp.rows.begin(), wp.rows.end());  // 0 / 1 as GF(2^8) cells
+      ent.wrows.assign(wp.rows.begin(), wp.rows.end());
     } else if (kind == KBITMATRIX) {
       const lio_erasure_plan_t *p = &e->pub;
       std::vector<int> bm(p->encode_bitmatrix, p->encode_bitmatrix + static_cast<size_t>(k) * p->parity_strips * p->w * p->w);
@@ -545,6 +549,8 @@ int decode_entry_locked(PlanExt *e, const std::vector<int> &ids, int dev, Decode
       uint32_t *d = nullptr;
       if (upload_masks(ent.masks, &d)) return -1;
       dm = ent.dev_masks.emplace(dev, d).first;
+      if (kind == KWORDWISE)
+        lsec::jit::bind_w(d, ent.wrows.data(), static_cast<int>(ent.dp.erased.size()), e->pub.data_strips, e->pub.w);
     }
     *out = &ent;
     *cells = dm->second;
@@ -597,19 +603,30 @@ int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
 // word products [(r*K + j)*w + b] (KWORDWISE / KBITSLICEDW), grouped when K > kMaxK.
 int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in, const ShardRef *out,
                   int nstripes, long long size, int packet, hipStream_t st, int w = 8) {
-  if (kind == KBYTEWISE && lsec::bytewise_variant() == 0 && lsec::jit::wants_xornet(R, K)) {
+  const bool net = kind == KBYTEWISE   ? lsec::bytewise_variant() == 0 && lsec::jit::wants_xornet(R, K)
+                   : kind == KWORDWISE ? lsec::bitsliced_variant() == 0 && lsec::jit::wants_gfw_net(R, K, w)
+                                       : false;
+  ShardRef tin[lsec::kMaxK], tout[lsec::kMaxR];  // a w = 16 / 32 network's ragged tail, below
+  if (net) {
     if (hipFunction_t fn = lsec::jit::ready(image, R, K)) {  // the matrix's compiled XOR network
+      // w = 16 / 32 networks take whole tiles only: the tail columns go to the generic kernel
+      const long long whole = kind == KWORDWISE ? size / lsec::jit::gfw_tile(w) * lsec::jit::gfw_tile(w) : size;
       // batches split so tile indices stay 32-bit, as below
       const long long per = std::max(1LL, (1LL << 30) / std::max(1LL, size / 4096 + 1));
       ShardRef bi[lsec::jit::kMaxCols], bo[lsec::jit::kMaxRows];
-      for (int s0 = 0; s0 < nstripes; s0 += static_cast<int>(std::min<long long>(per, nstripes))) {
+      for (int s0 = 0; whole > 0 && s0 < nstripes; s0 += static_cast<int>(std::min<long long>(per, nstripes))) {
         const int n = static_cast<int>(std::min<long long>(per, nstripes - s0));
         for (int j = 0; j < K; ++j) bi[j] = {in[j].base + static_cast<uint64_t>(s0) * in[j].stride, in[j].stride};
         for (int r = 0; r < R; ++r) bo[r] = {out[r].base + static_cast<uint64_t>(s0) * out[r].stride, out[r].stride};
-        const hipError_t err = lsec::jit::launch(fn, R, K, bi, bo, n, size, st);
+        const hipError_t err = lsec::jit::launch(fn, R, K, bi, bo, n, whole, st, kind == KWORDWISE ? w : 8);
         if (err != hipSuccess) return fail("xor network launch failed: %s", hipGetErrorString(err));
       }
-      return 0;
+      if (whole == size) return 0;
+      for (int j = 0; j < K; ++j) tin[j] = {in[j].base + static_cast<uint64_t>(whole), in[j].stride};
+      for (int r = 0; r < R; ++r) tout[r] = {out[r].base + static_cast<uint64_t>(whole), out[r].stride};
+      in = tin;
+      out = tout;
+      size -= whole;
     }
   }
   const int rmax = kind == KBITMATRIX ? 2 : ((kind == KBITSLICEDW || kind == KWORDWISE) && w == 32) ? 4 : 8;
@@ -3562,6 +3579,7 @@ void et_destroy_plan(lio_erasure_plan_t *p) {
       (void)hipFree(kv.second);
     }
     for (auto &kv : e->impl->enc_dev_masks) {
+      lsec::jit::unbind(kv.second);
       (void)hipSetDevice(kv.first);
       (void)hipFree(kv.second);
     }
@@ -3572,6 +3590,7 @@ void et_destroy_plan(lio_erasure_plan_t *p) {
         (void)hipFree(kv.second);
       }
       for (auto &kv : ent.second.dev_masks) {
+        lsec::jit::unbind(kv.second);
         (void)hipSetDevice(kv.first);
         (void)hipFree(kv.second);
       }
@@ -3909,7 +3928,10 @@ int lsec_prepare_encode(lio_erasure_plan_t *plan) {
 
 int lsec_plan_jit(lio_erasure_plan_t *plan, const int *erasures) {
   PlanExt *e = ext_of(plan);
-  if (!e || kernel_kind(e->pub.method, e->pub.w) != KBYTEWISE || lsec::bytewise_variant() != 0) return 0;
+  if (!e) return 0;
+  const int kind = kernel_kind(e->pub.method, e->pub.w);
+  if (kind == KBYTEWISE ? lsec::bytewise_variant() != 0 : kind == KWORDWISE ? lsec::bitsliced_variant() != 0 : true)
+    return 0;
   const void *cells = nullptr;
   int R = 0;
   if (!erasures) {
@@ -3962,10 +3984,6 @@ int lsec_plan_kernel(lio_erasure_plan_t *plan) { return plan ? kernel_kind(plan-
 void lsec_set_kernel_variant(int bytewise_variant, int bitsliced_variant) {
   lsec::set_kernel_variant(bytewise_variant, bitsliced_variant);
 }
-
-// Tuning hook, not part of include/*.h: force the tile order of the bytewise and bit-sliced
-// kernels (ApplyArgs::order; -1 restores the default policy).
-void lsec_set_tile_order(int order) { lsec::set_tile_order(order); }
 
 int lsec_hbm_copy_dev(void *dst, const void *src, unsigned long long bytes, void *stream) {
   const hipError_t e = lsec::launch_hbm_copy(dst, src, bytes, static_cast<hipStream_t>(stream));

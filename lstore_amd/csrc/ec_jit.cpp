@@ -21,6 +21,14 @@
 // computes the same GF(2^8) products as the table kernel, bit for bit; it is used once its
 // compile has finished (in the background), and the table kernel serves until then.
 // LSEC_JIT=0 turns it off.
+//
+// RS / r6 at w = 16 / 32 (Jerasure's word layout, galois.c:527-604, :730-810) get the same
+// treatment in the bit-sliced domain of k_gfw_transposed: each lane transposes W words of an
+// input so that word x holds bit x of 32 elements, and output slice b of row r is the XOR of the
+// input slices x whose product c_rj * x^x has bit b set -- the 32 x 32 (16 x 16) bitmatrix block
+// of the coefficient, known at compile time, so every slice is a straight chain of 3-input XORs
+// (about w/4 per output slice per input) instead of the generic kernel's popcount(c) sweeps of
+// w XORs plus w-1 doublings.  gfw_source below.
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
@@ -63,11 +71,22 @@ std::string xor_chain(std::vector<std::string> t) {
 
 }  // namespace
 
-bool wants_xornet(int R, int K) {
+bool jit_on() {
   static const bool on = [] {
     const char *s = getenv("LSEC_JIT");
     return !s || *s != '0';
   }();
+  return on;
+}
+
+bool wants_gfw_net(int R, int K, int w) {
+  // every non-trivial w = 16 / 32 matrix (XOR-only ones take the plain-XOR path); at w = 32 the
+  // R x 32 accumulator slices limit a network to 4 rows, as the generic kernel's launches
+  return jit_on() && (w == 16 || w == 32) && R >= 1 && R <= (w == 32 ? 4 : kMaxRows) && K >= 1 && K <= kMaxCols;
+}
+
+bool wants_xornet(int R, int K) {
+  const bool on = jit_on();
   static const int min_cells = [] {  // LSEC_JIT_MIN: smallest R * K served by a network (A/B runs)
     const char *s = getenv("LSEC_JIT_MIN");
     return s ? atoi(s) : 96;
@@ -257,6 +276,178 @@ std::string xornet_source(const uint8_t *mat, int R, int K) {
   return s.str();
 }
 
+// ---- GF(2^16) / GF(2^32): bit-sliced networks over Jerasure's word layout
+namespace {
+
+// c * x in GF(2^w), Jerasure's polynomials (galois.c:65-98: 0210013, 020000007)
+uint32_t gfw_times_x(uint32_t c, int w) {
+  if (w == 16) {
+    c <<= 1;
+    return (c & 0x10000u) ? (c ^ 0x1100Bu) & 0xFFFFu : c;
+  }
+  const bool top = c >> 31;
+  return (c << 1) ^ (top ? 0x400007u : 0u);
+}
+
+// Greedy common-pair elimination (Paar) over one input's rows (sets of slice ids 0..W-1):
+// at most `cap` shared pairs, each used by at least 3 rows.  New symbols are W, W+1, ...
+void share_slice_pairs(std::vector<std::vector<int>> &rows, int W, int cap, std::vector<std::pair<int, int>> &pairs) {
+  while (static_cast<int>(pairs.size()) < cap) {
+    const int nsym = W + static_cast<int>(pairs.size());
+    std::vector<int> count(static_cast<size_t>(nsym) * nsym, 0);
+    for (auto &row : rows)
+      for (size_t i = 0; i < row.size(); ++i)
+        for (size_t j = i + 1; j < row.size(); ++j) {
+          const int a = std::min(row[i], row[j]), b = std::max(row[i], row[j]);
+          ++count[static_cast<size_t>(a) * nsym + b];
+        }
+    int best = -1, n = 0;
+    for (size_t i = 0; i < count.size(); ++i)
+      if (count[i] > n) {
+        n = count[i];
+        best = static_cast<int>(i);
+      }
+    if (n < 3) return;
+    const int a = best / nsym, b = best % nsym;
+    pairs.push_back({a, b});
+    for (auto &row : rows) {
+      auto ia = std::find(row.begin(), row.end(), a), ib = std::find(row.begin(), row.end(), b);
+      if (ia == row.end() || ib == row.end()) continue;
+      row.erase(std::remove_if(row.begin(), row.end(), [&](int x) { return x == a || x == b; }), row.end());
+      row.push_back(nsym);
+    }
+  }
+}
+
+}  // namespace
+
+int gfw_tile(int w) { return 256 * 4 * w; }
+
+std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
+  // LSEC_JIT_VARIANT bits 8-15: most shared pairs per input (0: the default 32, 255: none);
+  // bit 16: let the compiler schedule loads freely (no one-input-ahead prefetch fenced by sched
+  // barriers: it then hoists every input's loads and spills at 10+4, w = 32)
+  const int capv = (jit_variant() >> 8) & 255;
+  const int cap = capv == 0 ? 32 : capv == 255 ? 0 : capv;
+  const bool fenced = !((jit_variant() >> 16) & 1);
+  const int tile = gfw_tile(W);  // the launch covers whole tiles only
+  std::ostringstream s;
+  s << "typedef unsigned int u32;\n"
+       "typedef u32 u32x4 __attribute__((ext_vector_type(4)));\n"
+       "typedef u32 u32x2 __attribute__((ext_vector_type(2)));\n"
+       "struct Ref { unsigned long long base; long long stride; };\n"
+    << "struct Args { long long size; int nstripes; int pad; Ref in[" << K << "]; Ref out[" << R << "]; };\n"
+    << "#define W " << W << "\n"
+       "#define X3(a,b,c) __builtin_amdgcn_bitop3_b32((a),(b),(c),0x96)\n"
+       "#define G(a) ((const __attribute__((address_space(1))) u32x4 *)(a))\n"
+       "#define GW(a) ((__attribute__((address_space(1))) u32x4 *)(a))\n"
+       "#define G2(a) ((const __attribute__((address_space(1))) u32x2 *)(a))\n"
+       "#define GW2(a) ((__attribute__((address_space(1))) u32x2 *)(a))\n"
+       // the W x W bit transpose of k_gfw_transposed (ec_kernels_impl.h, transpose_units)
+       "template <int d> __device__ static inline void tb(u32 (&D)[W], u32 m) {\n"
+       "#pragma unroll\n"
+       "  for (int r = 0; r < W; ++r) { if (r & d) continue; const u32 x = D[r], y = D[r + d];\n"
+       "    D[r] = (x & m) | ((y << d) & ~m); D[r + d] = ((x >> d) & m) | (y & ~m); }\n"
+       "}\n"
+       "__device__ static inline void tr(u32 (&D)[W]) {\n"
+       "#if W == 32\n"
+       "#pragma unroll\n"
+       "  for (int r = 0; r < 16; ++r) { const u32 x = D[r], y = D[r + 16];\n"
+       "    D[r] = __builtin_amdgcn_perm(y, x, 0x05040100u); D[r + 16] = __builtin_amdgcn_perm(y, x, 0x07060302u); }\n"
+       "#endif\n"
+       "#pragma unroll\n"
+       "  for (int r = 0; r < W; ++r) { if (r & 8) continue; const u32 x = D[r], y = D[r + 8];\n"
+       "    D[r] = __builtin_amdgcn_perm(y, x, 0x06020400u); D[r + 8] = __builtin_amdgcn_perm(y, x, 0x07030501u); }\n"
+       "  tb<4>(D, 0x0F0F0F0Fu); tb<2>(D, 0x33333333u); tb<1>(D, 0x55555555u);\n"
+       "}\n"
+       // a lane's W dwords of a shard: W/4 pieces of 16 B, 4 KiB apart.  Whole tiles only: the
+       // launcher hands a ragged tail to the generic kernel, so loads are unconditional and each
+       // tile is one basic block for the scheduler
+       "__device__ static inline void ld(u32 (&e)[W], unsigned long long p) {\n"
+       "#pragma unroll\n"
+       "  for (int q = 0; q < W / 4; ++q) { const u32x4 v = __builtin_nontemporal_load(G(p + q * 4096));\n"
+       "    e[4 * q] = v.x; e[4 * q + 1] = v.y; e[4 * q + 2] = v.z; e[4 * q + 3] = v.w; }\n"
+       "}\n"
+       "__device__ static inline void st(const u32 (&h)[W], unsigned long long p) {\n"
+       "#pragma unroll\n"
+       "  for (int q = 0; q < W / 4; ++q)\n"
+       "    __builtin_nontemporal_store((u32x4){h[4 * q], h[4 * q + 1], h[4 * q + 2], h[4 * q + 3]}, GW(p + q * 4096));\n"
+       "}\n"
+       "extern \"C\" __global__ __launch_bounds__(256) void lsec_xornet(Args a) {\n"
+       "  const long long C = a.size;\n"
+    << "  const unsigned tps = (unsigned)(C / " << tile << ");\n"
+    << "  const unsigned nt = tps * (unsigned)a.nstripes;\n"
+       "  const unsigned nb = gridDim.x, per = nb >> 3, rem = nb & 7, xcd = blockIdx.x & 7;\n"
+       "  const unsigned t0 = xcd * per + (xcd < rem ? xcd : rem) + (blockIdx.x >> 3);\n"
+       "  for (unsigned t = t0; t < nt; t += nb) {\n"
+       "    const unsigned s = t / tps;\n"
+    << "    const long long base = (long long)(t - s * tps) * " << tile << " + threadIdx.x * 16;\n";
+  for (int r = 0; r < R; ++r) s << "    u32 h" << r << "[W];\n";
+  std::vector<std::vector<bool>> live(R, std::vector<bool>(W, false));
+  // inputs with a non-zero coefficient in some row, each loaded one input ahead of its use: the
+  // scheduler would otherwise hoist every input's loads to the top (K x W registers live: spills
+  // at 10+4, w = 32), so sched barriers fence each input's arithmetic
+  std::vector<int> used;
+  for (int j = 0; j < K; ++j)
+    for (int r = 0; r < R; ++r)
+      if (mat[r * K + j]) {
+        used.push_back(j);
+        break;
+      }
+  auto load = [&](size_t u) {
+    const int j = used[u];
+    s << "    ld(e" << (u & 1) << ", a.in[" << j << "].base + (unsigned long long)s * a.in[" << j << "].stride + base);\n";
+  };
+  s << "    u32 e0[W], e1[W];\n";
+  if (!used.empty()) load(0);
+  for (size_t u = 0; u < used.size(); ++u) {
+    const int j = used[u];
+    if (u + 1 < used.size()) load(u + 1);
+    // the bitmatrix block of every row's coefficient c_rj: slice b of the output takes input
+    // slices x with bit b of c_rj * x^x set
+    std::vector<std::vector<int>> rows(static_cast<size_t>(R) * W);
+    bool any = false;
+    for (int r = 0; r < R; ++r) {
+      uint32_t cx = mat[r * K + j];
+      for (int x = 0; x < W && cx; ++x) {
+        for (int b = 0; b < W; ++b)
+          if ((cx >> b) & 1u) rows[static_cast<size_t>(r) * W + b].push_back(x);
+        cx = gfw_times_x(cx, W);
+      }
+      any |= mat[r * K + j] != 0;
+    }
+    (void)any;
+    std::vector<std::pair<int, int>> pairs;
+    if (cap > 0) share_slice_pairs(rows, W, cap, pairs);
+    s << "    { u32 (&e)[W] = e" << (u & 1) << ";\n      tr(e);\n";
+    for (size_t i = 0; i < pairs.size(); ++i) {
+      auto nm = [&](int x) { return x < W ? "e[" + std::to_string(x) + "]" : "p" + std::to_string(x - W); };
+      s << "      const u32 p" << i << " = " << nm(pairs[i].first) << " ^ " << nm(pairs[i].second) << ";\n";
+    }
+    for (int r = 0; r < R; ++r)
+      for (int b = 0; b < W; ++b) {
+        const auto &row = rows[static_cast<size_t>(r) * W + b];
+        if (row.empty()) continue;
+        std::vector<std::string> t;
+        const std::string acc = "h" + std::to_string(r) + "[" + std::to_string(b) + "]";
+        if (live[r][b]) t.push_back(acc);
+        for (int x : row) t.push_back(x < W ? "e[" + std::to_string(x) + "]" : "p" + std::to_string(x - W));
+        s << "      " << acc << " = " << xor_chain(t) << ";\n";
+        live[r][b] = true;
+      }
+    s << "    }\n";
+    if (fenced) s << "    __builtin_amdgcn_sched_barrier(0);\n";
+  }
+  for (int r = 0; r < R; ++r) {
+    for (int b = 0; b < W; ++b)
+      if (!live[r][b]) s << "    h" << r << "[" << b << "] = 0u;\n";
+    s << "    tr(h" << r << ");\n    st(h" << r << ", a.out[" << r << "].base + (unsigned long long)s * a.out[" << r
+      << "].stride + base);\n";
+  }
+  s << "  }\n}\n";
+  return s.str();
+}
+
 int xornet_tile(int K) {
   int D = (jit_variant() >> 4) & 15;
   if (D != 1 && D != 2 && D != 4) D = 4;
@@ -267,8 +458,8 @@ int xornet_tile(int K) {
 namespace {
 
 struct Entry {
-  std::vector<uint8_t> mat;
-  int R = 0, K = 0;
+  std::vector<uint32_t> mat;  // R x K coefficients (GF(2^w) elements)
+  int R = 0, K = 0, w = 8;
   enum State { kCompiling, kReady, kFailed } state = kCompiling;
   std::vector<char> code;                 // code object
   std::map<int, hipModule_t> modules;     // device -> module
@@ -288,19 +479,26 @@ void drain_compiles() {
   std::unique_lock<std::mutex> lk(g_mu);
   g_cv.wait_for(lk, std::chrono::seconds(2), [] { return g_compiling == 0; });
 }
-auto &g_by_matrix = *new std::map<std::vector<uint8_t>, std::shared_ptr<Entry>>();  // key: R, K, matrix
+auto &g_by_matrix = *new std::map<std::vector<uint32_t>, std::shared_ptr<Entry>>();  // key: R, K, w, matrix
 auto &g_by_image = *new std::map<const void *, std::shared_ptr<Entry>>();           // device image -> entry
 
-std::vector<uint8_t> key_of(const uint8_t *mat, int R, int K) {
-  std::vector<uint8_t> k(2 + static_cast<size_t>(R) * K);
-  k[0] = static_cast<uint8_t>(R);
-  k[1] = static_cast<uint8_t>(K);
-  std::memcpy(k.data() + 2, mat, static_cast<size_t>(R) * K);
+std::vector<uint32_t> key_of(const uint32_t *mat, int R, int K, int w) {
+  std::vector<uint32_t> k(3 + static_cast<size_t>(R) * K);
+  k[0] = static_cast<uint32_t>(R);
+  k[1] = static_cast<uint32_t>(K);
+  k[2] = static_cast<uint32_t>(w);
+  std::memcpy(k.data() + 3, mat, sizeof(uint32_t) * R * K);
   return k;
 }
 
 void compile(std::shared_ptr<Entry> e) {
-  const std::string src = xornet_source(e->mat.data(), e->R, e->K);
+  std::string src;
+  if (e->w == 8) {
+    std::vector<uint8_t> m8(e->mat.begin(), e->mat.end());
+    src = xornet_source(m8.data(), e->R, e->K);
+  } else {
+    src = gfw_source(e->mat.data(), e->R, e->K, e->w);
+  }
   hiprtcProgram prog = nullptr;
   std::string err;
   std::vector<char> code;
@@ -324,7 +522,7 @@ void compile(std::shared_ptr<Entry> e) {
   }
   static const bool trace = getenv("LSEC_TRACE") != nullptr;
   if (trace || !err.empty())
-    fprintf(stderr, "[lsec jit] %dx%d xor network: %s\n", e->R, e->K, err.empty() ? "compiled" : err.c_str());
+    fprintf(stderr, "[lsec jit] %dx%d w=%d xor network: %s\n", e->R, e->K, e->w, err.empty() ? "compiled" : err.c_str());
   std::lock_guard<std::mutex> lk(g_mu);
   e->code.swap(code);
   e->err = err;
@@ -355,17 +553,28 @@ hipFunction_t function_locked(Entry &e, int dev) {
 
 void bind(const void *image, const uint8_t *mat, int R, int K) {
   if (!image || !wants_xornet(R, K)) return;
+  std::vector<uint32_t> m32(mat, mat + static_cast<size_t>(R) * K);
+  bind_entry(image, m32.data(), R, K, 8);
+}
+
+void bind_w(const void *image, const uint32_t *mat, int R, int K, int w) {
+  if (!image || !wants_gfw_net(R, K, w)) return;
+  bind_entry(image, mat, R, K, w);
+}
+
+void bind_entry(const void *image, const uint32_t *mat, int R, int K, int w) {
   std::shared_ptr<Entry> e;
   bool start = false;
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    const std::vector<uint8_t> key = key_of(mat, R, K);
+    const std::vector<uint32_t> key = key_of(mat, R, K, w);
     auto it = g_by_matrix.find(key);
     if (it == g_by_matrix.end()) {
       e = std::make_shared<Entry>();
       e->mat.assign(mat, mat + static_cast<size_t>(R) * K);
       e->R = R;
       e->K = K;
+      e->w = w;
       g_by_matrix.emplace(key, e);
       start = true;
       ++g_compiling;
@@ -426,7 +635,7 @@ hipFunction_t ready(const void *image, int R, int K) {
 }
 
 hipError_t launch(hipFunction_t fn, int R, int K, const ShardRef *in, const ShardRef *out, int nstripes, int64_t size,
-                  hipStream_t st) {
+                  hipStream_t st, int w) {
   // struct Args { long long size; int nstripes; int pad; Ref in[K]; Ref out[R]; }
   std::vector<uint8_t> args(16 + sizeof(ShardRef) * (K + R));
   std::memcpy(args.data(), &size, 8);
@@ -435,7 +644,7 @@ hipError_t launch(hipFunction_t fn, int R, int K, const ShardRef *in, const Shar
   std::memcpy(args.data() + 16 + sizeof(ShardRef) * K, out, sizeof(ShardRef) * R);
   size_t bytes = args.size();
   void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes, HIP_LAUNCH_PARAM_END};
-  const int64_t tile = xornet_tile(K);  // as xornet_source
+  const int64_t tile = w == 8 ? xornet_tile(K) : gfw_tile(w);  // as xornet_source / gfw_source
   const uint64_t ntiles = static_cast<uint64_t>((size + tile - 1) / tile) * static_cast<uint64_t>(nstripes);
   if (ntiles == 0) return hipSuccess;
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;

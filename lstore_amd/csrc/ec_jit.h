@@ -17,8 +17,14 @@ constexpr int kMaxCols = 32;  // input columns (registers: 8 slices per input pe
 
 // whether an R x K bytewise matrix is served by a network (wide codes only; LSEC_JIT=0: never)
 bool wants_xornet(int R, int K);
+// whether an R x K GF(2^w) matrix (w = 16 / 32, word layout) is served by a network
+bool wants_gfw_net(int R, int K, int w);
 // HIP source of the network for the row-major R x K matrix (exposed for tests and tools)
 std::string xornet_source(const uint8_t *mat, int R, int K);
+// HIP source of the bit-sliced network for an R x K GF(2^w) matrix, w = 16 / 32
+std::string gfw_source(const uint32_t *mat, int R, int K, int w);
+// bytes of a shard one block of a w = 16 / 32 network covers per tile; it serves whole tiles only
+int gfw_tile(int w);
 // bytes of a shard one 256-lane block of the network covers per tile
 int xornet_tile(int K);
 // LSEC_JIT_VARIANT (code shape knobs for A/B runs; 0 = default)
@@ -26,15 +32,18 @@ int jit_variant();
 // Associate a device coefficient image with its matrix and start compiling that matrix's
 // network in the background (once per matrix per process).  unbind before the image is freed.
 void bind(const void *image, const uint8_t *mat, int R, int K);
+void bind_w(const void *image, const uint32_t *mat, int R, int K, int w);  // w = 16 / 32
+void bind_entry(const void *image, const uint32_t *mat, int R, int K, int w);
 void unbind(const void *image);
 // Block until the image's network is compiled (or failed, or timeout): 1 ready, 0 otherwise
 // (also 0 when the image has no network).
 int wait(const void *image, int timeout_ms);
 // The compiled network for `image` on the current device, or nullptr (not bound / not ready).
 hipFunction_t ready(const void *image, int R, int K);
-// out[r] = sum_j A[r][j] in[j] for every stripe (same shard addressing as ApplyArgs).
+// out[r] = sum_j A[r][j] in[j] for every stripe (same shard addressing as ApplyArgs); at
+// w = 16 / 32 over the first size / gfw_tile(w) whole tiles of every shard only.
 hipError_t launch(hipFunction_t fn, int R, int K, const ShardRef *in, const ShardRef *out, int nstripes, int64_t size,
-                  hipStream_t st);
+                  hipStream_t st, int w = 8);
 
 }  // namespace jit
 }  // namespace lsec

@@ -64,7 +64,6 @@ struct ApplyArgs {
                           // wordwise: R x K x w products, [(r*K + j)*w + b] = c_rj * x^b
   int w;                  // bitmatrix: packets per super-packet; wordwise: field width (16 / 32)
   int accumulate;         // 1: out[r] ^= the result (the second and later input groups of a wide stripe)
-  int order;              // tile order (bytewise / bitsliced): 0 = stripe-major, else see tile_at (set by the launcher)
   unsigned long long *magic_acc;  // encode only (bytewise, bitsliced): fused stripe magic over the K inputs then the
                                   // R outputs (2 x u64 per stripe, zeroed), see MagicArgs
   ShardRef in[kMaxK];
@@ -170,7 +169,7 @@ void make_word_cell(uint32_t c, int w, uint32_t *out);
 
 // Variant selection knobs for experiments: 0 = default
 void set_kernel_variant(int bytewise_variant, int bitsliced_variant);
-void set_tile_order(int order);  // -1: default policy; else ApplyArgs::order for every launch (A/B runs)
 int bytewise_variant();  // != 0: a forced bytewise shape (also keeps wide codes off their XOR networks)
+int bitsliced_variant();  // != 0: a forced bit-sliced / wordwise variant (also keeps w = 16 / 32 RS off its XOR network)
 
 }  // namespace lsec

@@ -10,13 +10,6 @@ namespace lsec {
 namespace {
 
 int g_bw_variant = 0, g_bs_variant = 0;
-int g_tile_order = -1;  // -1: the default policy (tile_order below); else forced (lsec_set_tile_order)
-
-// Tile order of the bytewise and bitsliced kernels (ApplyArgs::order, tile_at).
-int tile_order(const ApplyArgs &a) {
-  if (g_tile_order >= 0) return g_tile_order;
-  return 0;
-}
 
 int default_grid(uint64_t ntiles) {
   // One tile per block: on this streaming pattern a full grid beat every grid-stride
@@ -64,9 +57,8 @@ void set_kernel_variant(int bw, int bs) {
   g_bs_variant = bs;
 }
 
-void set_tile_order(int order) { g_tile_order = order; }
-
 int bytewise_variant() { return g_bw_variant; }
+int bitsliced_variant() { return g_bs_variant; }
 
 hipError_t launch_bytewise(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
   if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > 8 || a.size % 8 != 0) return hipErrorInvalidValue;
@@ -76,9 +68,7 @@ hipError_t launch_bytewise(const ApplyArgs &a, hipStream_t st, int grid_blocks) 
   const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);
-  ApplyArgs b = a;
-  b.order = tile_order(a);
-  return by_r(a.R, [&](auto r) { return dispatch_bytewise<decltype(r)::value>(b, st, grid, shape); });
+  return by_r(a.R, [&](auto r) { return dispatch_bytewise<decltype(r)::value>(a, st, grid, shape); });
 }
 
 hipError_t launch_bytewise_magic(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
@@ -88,9 +78,7 @@ hipError_t launch_bytewise_magic(const ApplyArgs &a, hipStream_t st, int grid_bl
   const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);
-  ApplyArgs b = a;
-  b.order = tile_order(a);
-  return by_r(a.R, [&](auto r) { return dispatch_bytewise_magic<decltype(r)::value>(b, st, grid); });
+  return by_r(a.R, [&](auto r) { return dispatch_bytewise_magic<decltype(r)::value>(a, st, grid); });
 }
 
 hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
@@ -105,9 +93,7 @@ hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid_blocks)
   const uint64_t ntiles = ((col_bytes + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   const int grid = grid_blocks > 0 ? grid_blocks : default_grid(ntiles);
-  ApplyArgs b = a;
-  b.order = tile_order(a);
-  return by_r(a.R, [&](auto r) { return dispatch_bitsliced<decltype(r)::value>(b, st, grid, dw); });
+  return by_r(a.R, [&](auto r) { return dispatch_bitsliced<decltype(r)::value>(a, st, grid, dw); });
 }
 
 bool bitmatrix_w_supported(int w) {

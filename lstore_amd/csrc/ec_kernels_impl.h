@@ -100,29 +100,6 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
   return xcd * per + min(xcd, rem) + (b >> 3);
 }
 
-// Tile t of a launch -> (stripe, column tile of that stripe).  order = G | rot << 8:
-//   G <= 1   stripe-major: a stripe's column tiles are consecutive (the default)
-//   G > 1    groups of G stripes, column-major inside a group: blocks running together cover
-//            the same columns of G stripes instead of a long run of one stripe's columns
-//   rot      column tiles of stripe s start at tile (s * rot) mod tps (a rotation per stripe)
-//   bit 16   no XCD-contiguous remap of block ids
-// A speed hint only: every (stripe, column tile) is visited exactly once whatever the order.
-constexpr int kOrderNoRemap = 1 << 16;  // order bit: blocks take tiles in launch order (no XCD remap)
-__device__ __forceinline__ uint32_t tile_at(uint32_t t, uint32_t tps, uint32_t nst, uint32_t order, uint32_t &col) {
-  const uint32_t G = order & 255u, rot = (order >> 8) & 255u;
-  uint32_t s;
-  if (G <= 1) {
-    s = t / tps;
-    col = t - s * tps;
-  } else {
-    const uint32_t span = G * tps, g = t / span, s0 = g * G, gs = min(G, nst - s0), r = t - g * span;
-    col = r / gs;
-    s = s0 + (r - col * gs);
-  }
-  if (rot) col = (col + s * rot) % tps;
-  return s;
-}
-
 // ------------------------------------------------------------------ adler32 partial sums
 constexpr uint32_t kAdlerMod = 65521;
 
@@ -347,11 +324,10 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
   const uint32_t ntiles = tiles_per_stripe * static_cast<uint32_t>(a.nstripes);
   ConstCell *cells = const_cells(a.cells);
 
-  for (uint32_t t = (a.order & kOrderNoRemap) ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
-    uint32_t ct;
-    const uint32_t s = tile_at(t, tiles_per_stripe, static_cast<uint32_t>(a.nstripes), static_cast<uint32_t>(a.order), ct);
-    const int64_t off0 = static_cast<int64_t>(ct) * kTile + threadIdx.x * kLane;
-    const bool full = (static_cast<int64_t>(ct) + 1) * kTile <= C;  // wave-uniform
+  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+    const uint32_t s = t / tiles_per_stripe;
+    const int64_t off0 = static_cast<int64_t>(t - s * tiles_per_stripe) * kTile + threadIdx.x * kLane;
+    const bool full = (static_cast<int64_t>(t - s * tiles_per_stripe) + 1) * kTile <= C;  // wave-uniform
 
     V acc[IT][R];
 #pragma unroll
@@ -487,10 +463,9 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
   const uint32_t ntiles = tiles_per_stripe * static_cast<uint32_t>(a.nstripes);
   ConstCell *cells = const_cells(a.cells);
 
-  for (uint32_t t = (a.order & kOrderNoRemap) ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
-    uint32_t ct;
-    const uint32_t s = tile_at(t, tiles_per_stripe, static_cast<uint32_t>(a.nstripes), static_cast<uint32_t>(a.order), ct);
-    const uint32_t colb = ct * kTile + threadIdx.x * (4 * DW);
+  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+    const uint32_t s = t / tiles_per_stripe;
+    const uint32_t colb = (t - s * tiles_per_stripe) * kTile + threadIdx.x * (4 * DW);
     // lanes past the end occur only in a ragged last tile (P % 16 == 0 keeps a lane's DW
     // dwords inside one packet); with MG they still join the block's magic reduction
     const bool valid = colb < col_bytes;

@@ -387,6 +387,47 @@ def test_xor_network_vs_oracle(cuda, k, m, size):
         assert np.array_equal(host, full)
 
 
+@pytest.mark.parametrize("method,k,m,w,size,lost", [
+    (L.REED_SOL_VAN, 6, 3, 16, 3 * 16384 + 40, [0, 1, 2]),   # ragged tail: the generic kernel finishes it
+    (L.REED_SOL_VAN, 6, 3, 32, 2 * 32768, [1, 6 + 1]),
+    (L.REED_SOL_VAN, 10, 4, 32, 2 * 32768 + 8, [0, 3, 5, 9]),
+    (L.REED_SOL_VAN, 10, 4, 16, 16384 + 16, [2, 10 + 2]),
+    (L.REED_SOL_VAN, 20, 6, 16, 16384 + 8, [0, 5, 7, 11, 13, 19]),
+    (L.REED_SOL_R6_OP, 6, 2, 32, 32768 + 24, [0, 4]),
+    (L.REED_SOL_VAN, 4, 2, 32, 8, [0, 1]),                  # smaller than one tile: generic kernel only
+])
+def test_gfw_network_vs_oracle(cuda, method, k, m, w, size, lost):
+    """RS / r6 at w = 16 / 32 run on their compiled bit-sliced XOR networks (ec_jit.cpp,
+    gfw_source) once prepared: encode and a dense decode bit-exact vs the oracle restatement
+    (pinned to the reference fixtures), device-resident and from host memory, with ragged tails
+    and all-0xFF stripes (every reduction tap used)."""
+    import torch
+
+    n = 3
+    rng = np.random.default_rng(k * w + m)
+    st = np.zeros((n, k + m, size), dtype=np.uint8)
+    st[:, :k] = rng.integers(0, 256, (n, k, size), dtype=np.uint8)
+    st[1, :k] = 0xFF
+    with L.Plan.new(method, size, k, m, w, 8, 8) as p:
+        assert p.form_encoding_matrix() == 0 and p.form_decoding_matrix() == 0
+        p.prepare_encode()
+        p.prepare_decode(lost)
+        assert p.jit() == 1 and p.jit(lost) == 1, "network not compiled"
+        want = np.stack([O.encode(method, st[s, :k], m, 0, w) for s in range(n)])
+        R = 2 if method == L.REED_SOL_R6_OP else m
+        data = torch.from_numpy(st[:, :k].copy()).cuda()
+        par = torch.full((n, m, size), 0x5A, dtype=torch.uint8, device="cuda")
+        p.encode_dev(data, par)
+        assert np.array_equal(par.cpu().numpy()[:, :R], want[:, :R])
+        host = st.copy()
+        p.encode_stripes(host)
+        assert np.array_equal(host[:, k:k + R], want[:, :R])
+        full = host.copy()
+        host[:, lost] = 0x33
+        p.decode_stripes(host, lost)
+        assert np.array_equal(host, full)
+
+
 def test_stripe_width_limits_are_errors(cuda):
     """k + m > 256 (LSEC_MAX_DEVS) is refused with a message, never written past a table."""
     k, m, size = 200, 57, 4096

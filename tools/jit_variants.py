@@ -19,19 +19,23 @@ def main():
     ap.add_argument("--km", default="20+6")
     ap.add_argument("--method", default="reed_sol_van")
     ap.add_argument("--variants", default="0,1,2,3,0x41,0x40")
+    ap.add_argument("--w", type=int, default=8)
     a = ap.parse_args()
     import oracle as O
     from lstore_amd import erasure as E
     k, m = (int(x) for x in a.km.split("+"))
-    M = np.array(O.coding_matrix(E.JE_METHOD_NAMES.index(a.method), k, m, 8)).reshape(m, k)
-    inp = f"{m} {k} " + " ".join(map(str, M.flatten()))
+    M = np.array(O.coding_matrix(E.JE_METHOD_NAMES.index(a.method), k, m, a.w), dtype=np.int64).reshape(m, k)
+    M &= (1 << a.w) - 1
+    if a.w == 32:
+        M = M[1:5]  # a network takes at most 4 rows at w = 32 (rows 1.. : the non-trivial ones)
+    inp = f"{M.shape[0]} {k} {a.w} " + " ".join(map(str, M.flatten()))
     os.makedirs(os.path.join(ROOT, "build", "jit"), exist_ok=True)
     for v in a.variants.split(","):
         v = int(v, 0)
         env = dict(os.environ, LSEC_JIT_VARIANT=str(v))
         src = subprocess.run([os.path.join(ROOT, "build", "jit_src")], input=inp, capture_output=True, text=True,
                              env=env, check=True).stdout
-        base = os.path.join(ROOT, "build", "jit", f"{a.method}_{k}_{m}_v{v:#x}")
+        base = os.path.join(ROOT, "build", "jit", f"{a.method}_{k}_{m}_w{a.w}_v{v:#x}")
         open(base + ".hip", "w").write(src)
         r = subprocess.run(["hipcc", "-c", "--offload-arch=gfx950", "-O3", "--cuda-device-only", "-S", "-include", "hip/hip_runtime.h",
                             "-Rpass-analysis=kernel-resource-usage", "-o", base + ".s", base + ".hip"],
