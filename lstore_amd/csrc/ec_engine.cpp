@@ -1374,8 +1374,7 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
     if (cb < align) cb = align;
     if (cb >= C) cb = C;
   }
-  const int nb_max = cb < C ? 1 : static_cast<int>(std::max<size_t>(1, std::min<size_t>(nstripes, budget / 2 / (per_col * C))));
-  const size_t slot_bytes = per_col * static_cast<size_t>(cb) * nb_max;
+  int nb_max = cb < C ? 1 : static_cast<int>(std::max<size_t>(1, std::min<size_t>(nstripes, budget / 2 / (per_col * C))));
   Staging *stg = acquire_staging(dev);
   if (!stg) return fail("cannot create staging streams");
   int rc = 0;
@@ -1425,6 +1424,28 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   // (profiles/r01_v28_host_trace.txt), but DMA of the same small registered runs is slower still:
   // kernel in + DMA out gave 17-30 GiB/s encode against 28-32 (profiles/r01_v28_kcopy_modes.txt).
   const bool out_by_kernel = by_kernel;
+  // A packed call that fits one staging batch would pack, copy in, compute, copy out and unpack
+  // one after the other.  From 2 MiB such calls are cut into 2-8 batches (of stripes, or of
+  // column blocks of a single stripe), so the copy pool packs batch b+1 while batch b is on PCIe.
+  static const int max_blocks = [] {  // LSEC_HOST_BLOCKS (A/B runs; 1 = one batch)
+    const char *v = getenv("LSEC_HOST_BLOCKS");
+    return v ? std::max(1, atoi(v)) : 8;
+  }();
+  if (!pinned && nb_max >= nstripes && cb == C) {
+    const int nblk = static_cast<int>(std::min<size_t>(max_blocks, (per_col * C * nstripes) >> 20));
+    if (nblk >= 2 && nstripes >= nblk) {
+      nb_max = (nstripes + nblk - 1) / nblk;
+    } else if (nblk >= 2) {
+      const long long per_stripe = (nblk + nstripes - 1) / nstripes;
+      const long long align = packet_kind(kind) ? static_cast<long long>(p->w) * p->packet_size : 8192;
+      const long long c = ((C + per_stripe - 1) / per_stripe + align - 1) / align * align;
+      if (c < C) {
+        cb = c;
+        nb_max = 1;
+      }
+    }
+  }
+  const size_t slot_bytes = per_col * static_cast<size_t>(cb) * nb_max;
   const auto t_loop0 = now();
   std::vector<DmaRun> runs;
 

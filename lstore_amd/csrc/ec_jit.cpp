@@ -330,6 +330,8 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
   const int capv = (jit_variant() >> 8) & 255;
   const int cap = capv == 0 ? 32 : capv == 255 ? 0 : capv;
   const bool fenced = !((jit_variant() >> 16) & 1);
+  // bits 17-18: inputs loaded ahead of their use (0: the default 1)
+  const int ahead = std::max(1, (jit_variant() >> 17) & 3);
   const int tile = gfw_tile(W);  // the launch covers whole tiles only
   std::ostringstream s;
   s << "typedef unsigned int u32;\n"
@@ -394,15 +396,16 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
         used.push_back(j);
         break;
       }
+  const size_t nbuf = static_cast<size_t>(ahead) + 1;
   auto load = [&](size_t u) {
     const int j = used[u];
-    s << "    ld(e" << (u & 1) << ", a.in[" << j << "].base + (unsigned long long)s * a.in[" << j << "].stride + base);\n";
+    s << "    ld(e" << u % nbuf << ", a.in[" << j << "].base + (unsigned long long)s * a.in[" << j << "].stride + base);\n";
   };
-  s << "    u32 e0[W], e1[W];\n";
-  if (!used.empty()) load(0);
+  for (size_t b = 0; b < nbuf; ++b) s << "    u32 e" << b << "[W];\n";
+  for (size_t u = 0; u < used.size() && u < static_cast<size_t>(ahead); ++u) load(u);
   for (size_t u = 0; u < used.size(); ++u) {
     const int j = used[u];
-    if (u + 1 < used.size()) load(u + 1);
+    if (u + ahead < used.size()) load(u + ahead);
     // the bitmatrix block of every row's coefficient c_rj: slice b of the output takes input
     // slices x with bit b of c_rj * x^x set
     std::vector<std::vector<int>> rows(static_cast<size_t>(R) * W);
@@ -419,7 +422,7 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
     (void)any;
     std::vector<std::pair<int, int>> pairs;
     if (cap > 0) share_slice_pairs(rows, W, cap, pairs);
-    s << "    { u32 (&e)[W] = e" << (u & 1) << ";\n      tr(e);\n";
+    s << "    { u32 (&e)[W] = e" << u % nbuf << ";\n      tr(e);\n";
     for (size_t i = 0; i < pairs.size(); ++i) {
       auto nm = [&](int x) { return x < W ? "e[" + std::to_string(x) + "]" : "p" + std::to_string(x - W); };
       s << "      const u32 p" << i << " = " << nm(pairs[i].first) << " ^ " << nm(pairs[i].second) << ";\n";

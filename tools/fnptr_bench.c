@@ -21,12 +21,18 @@
  *        FNPTR_REF=path  also time the reference: oracle/_ref/libjerasure_ref.so (test
  *                        infrastructure: the real jerasure behind erasure_tools.c's dispatch)
  *        FNPTR_ONLY_REF=1  time the reference only
+ *        FNPTR_SET_MB=n  the threads' buffers together hold n MiB of stripes, and each thread
+ *                        walks its own stripes round-robin, one per call (default: 4x the last-level
+ *                        caches of the CPUs this process may run on, so neither implementation works
+ *                        on cache-resident chunks; 0 = one stripe per thread, reused every call)
  *        FNPTR_VERIFY=1  (with FNPTR_REF) every timed engine call is checked: the chunks it writes
  *                        are overwritten before the call, and after it must equal the reference's
  *                        (parity for encode, the lost data chunk 0 for decode); the JSON line then
  *                        carries "verified" and "mismatches", and the exit status is 2 on any
  */
+#define _GNU_SOURCE
 #include <dlfcn.h>
+#include <sched.h>
 #include <pthread.h>
 #include <sys/resource.h>
 #include <stdio.h>
@@ -45,6 +51,8 @@ static int (*g_ref_decode)(void *, char **, int, int *);
 static int (*g_host_malloc)(void **, size_t, unsigned);
 static int (*g_host_free)(void *);
 static int g_chunk, g_decode, g_use_ref, g_verify, g_k = 6, g_m = 3;
+static long g_nbuf = 1;  /* stripes per thread (FNPTR_SET_MB) */
+static double g_set_mb;
 static long g_verified, g_mismatch;  /* FNPTR_VERIFY counters (atomic adds) */
 static double g_seconds;
 static volatile double g_t_end;
@@ -80,17 +88,21 @@ static void *worker(void *arg)
     thread_rec_t *r = (thread_rec_t *)arg;
     int k = g_k, m = g_m;
     char *buf = NULL;
+    const size_t stripe = (size_t)(k + m) * g_chunk;
+    const long nbuf = g_nbuf;
     if (g_host_malloc) {
-        if (g_host_malloc((void **)&buf, (size_t)(k + m) * g_chunk, 0) != 0) buf = NULL;
+        if (g_host_malloc((void **)&buf, stripe * nbuf, 0) != 0) buf = NULL;
     } else {
-        buf = malloc((size_t)(k + m) * g_chunk);
+        buf = malloc(stripe * nbuf);
     }
     char *ptr[256];
+    long cur = 0;
     int erasures[2] = {0, -1};
     char *gold = NULL;  /* FNPTR_VERIFY: the stripe with the reference's parity */
     const size_t C = (size_t)g_chunk;
     if (buf) {
-        for (size_t i = 0; i < (size_t)(k + m) * g_chunk; i++) buf[i] = (char)(i * 131 + r->t);
+        for (size_t i = 0; i < stripe; i++) buf[i] = (char)(i * 131 + r->t);
+        for (long b = 1; b < nbuf; b++) memcpy(buf + b * stripe, buf, stripe);  /* every page touched */
         for (int i = 0; i < k + m; i++) ptr[i] = buf + (size_t)i * g_chunk;
         if (g_use_ref || g_verify) g_ref_encode(g_ref, ptr, g_chunk);   /* consistent parity for the decodes */
         else g_plan->encode_block(g_plan, ptr, g_chunk);
@@ -102,6 +114,10 @@ static void *worker(void *arg)
     }
     pthread_barrier_wait(&g_bar);  /* timed phase starts */
     while (buf) {
+        if (nbuf > 1) {  /* the next stripe of this thread's set */
+            cur = cur + 1 == nbuf ? 0 : cur + 1;
+            for (int i = 0; i < k + m; i++) ptr[i] = buf + cur * stripe + (size_t)i * g_chunk;
+        }
         if (gold) {  /* overwrite what the call must write */
             if (g_decode) memset(ptr[0], 0xA5, C);
             else memset(ptr[k], 0x5A, (size_t)m * C);
@@ -125,6 +141,38 @@ static void *worker(void *arg)
     }
     free(gold);
     return NULL;
+}
+
+/* total last-level cache of the CPUs this process may run on (distinct index3 domains), bytes */
+static double llc_bytes(void)
+{
+    cpu_set_t set;
+    char seen[64][256];
+    int nseen = 0;
+    double total = 0;
+    if (sched_getaffinity(0, sizeof(set), &set) != 0) return 256.0 * (1 << 20);
+    for (int c = 0; c < CPU_SETSIZE; c++) {
+        if (!CPU_ISSET(c, &set)) continue;
+        char path[128], dom[256] = {0}, size[64] = {0};
+        snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", c);
+        FILE *f = fopen(path, "r");
+        if (!f) continue;
+        if (!fgets(dom, sizeof(dom), f)) dom[0] = 0;
+        fclose(f);
+        int dup = 0;
+        for (int i = 0; i < nseen && !dup; i++) dup = strcmp(seen[i], dom) == 0;
+        if (dup || nseen == 64) continue;
+        strcpy(seen[nseen++], dom);
+        snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/cache/index3/size", c);
+        if ((f = fopen(path, "r"))) {
+            if (fgets(size, sizeof(size), f)) {
+                double v = atof(size);
+                total += strchr(size, 'M') ? v * (1 << 20) : strchr(size, 'K') ? v * 1024 : v;
+            }
+            fclose(f);
+        }
+    }
+    return total > 0 ? total : 256.0 * (1 << 20);
 }
 
 static int cmp(const void *a, const void *b)
@@ -158,6 +206,9 @@ static void run(int T, const char *impl, const char *method)
 {
     pthread_t th[1024];
     thread_rec_t rec[1024];
+    const double stripe = (double)(g_k + g_m) * g_chunk;
+    g_nbuf = g_verify ? 1 : (long)(g_set_mb * (1 << 20) / (T * stripe));
+    if (g_nbuf < 1) g_nbuf = 1;
     pthread_barrier_init(&g_bar, NULL, T + 1);
     for (long t = 0; t < T; t++) {
         rec[t].t = t;
@@ -194,11 +245,12 @@ static void run(int T, const char *impl, const char *method)
            "\"method\": \"%s\", \"pinned\": %d, \"small_path\": \"%s\", \"per_call_us_p50\": %.1f, "
            "\"per_call_us_p99\": %.1f, \"per_call_us_p999\": %.1f, \"per_call_us_max\": %.1f, \"per_call_us_mean\": %.1f, "
            "\"gibps\": %.3f, \"cpu_util\": %.2f, \"cpu_us_per_call\": %.1f, \"cgroup_throttled_ms\": %.1f, "
-           "\"verified\": %ld, \"mismatches\": %ld}\n",
+           "\"verified\": %ld, \"mismatches\": %ld, \"stripes_per_thread\": %ld, \"set_mib\": %.0f}\n",
            impl, g_decode ? "decode" : "encode", g_chunk, T, calls, wall, method, g_host_malloc != NULL, sp ? sp : "default",
            n ? lat[n / 2] * 1e6 : 0.0, n ? lat[(size_t)(n * 0.99)] * 1e6 : 0.0, n ? lat[(size_t)(n * 0.999)] * 1e6 : 0.0,
            n ? lat[n - 1] * 1e6 : 0.0, n ? sum / n * 1e6 : 0.0, calls * (double)g_k * g_chunk / wall / (1 << 30),
-           cpu / wall, calls ? cpu / calls * 1e6 : 0.0, thr * 1e3, g_verified, g_mismatch);
+           cpu / wall, calls ? cpu / calls * 1e6 : 0.0, thr * 1e3, g_verified, g_mismatch, g_nbuf,
+           g_nbuf * (double)T * stripe / (1 << 20));
     fflush(stdout);
     free(lat);
 }
@@ -221,6 +273,8 @@ int main(int argc, char **argv)
     g_seconds = argc > 3 ? atof(argv[3]) : 2.0;
     int method = argc > 4 ? et_method_type(argv[4]) : CAUCHY_GOOD;
     g_decode = argc > 5 && strcmp(argv[5], "decode") == 0;
+    const char *set_mb = getenv("FNPTR_SET_MB");
+    g_set_mb = set_mb ? atof(set_mb) : 4 * llc_bytes() / (1 << 20);
     if (T > 1024) T = 1024;
     if (T < 1) T = 1;
     g_plan = et_generate_plan((long long)g_k * g_chunk, method, g_k, g_m, -1, -1, -1);   /* :2237 */
