@@ -1060,9 +1060,7 @@ struct CallerPinned {
 
 CallerPinned caller_pinned(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
                            long long C, bool kernel_ok) {
-  static const bool off = getenv("LSEC_NO_PINNED_DMA") != nullptr;
   CallerPinned r;
-  if (off) return r;
   // A first chunk that is not page-locked settles it, with no lock: every path below returns
   // "not pinned" for it too, and taking memory for pageable is always safe.  (Per-stripe calls
   // from hundreds of threads queued on this mutex.)
@@ -1623,13 +1621,8 @@ int device_layout(const lio_erasure_plan_t *p, char **ptrs, int nstripes, std::v
     // A single-stripe call (LStore's per-stripe fn-pointer path) stops at its first chunk:
     // every extra query is a turn on a runtime lock that spins, and at 128 threads on 16 CPUs
     // one extra query per call cut 16 KiB decodes from 30.2 to 3.2-5.3 GiB/s with the CPU quota
-    // spent spinning (profiles/r02_v32_zc_decode2.txt).  LSEC_PTR_CHECK=all checks its last chunk
-    // too.
-    static const bool check_all = [] {
-      const char *v = getenv("LSEC_PTR_CHECK");
-      return v && strcmp(v, "all") == 0;
-    }();
-    if (!check_all && nstripes == 1) return 0;
+    // spent spinning (profiles/r02_v32_zc_decode2.txt).
+    if (nstripes == 1) return 0;
     for (int s : {0, nstripes - 1})
       for (int i : {0, km - 1})
         if (is_device_ptr(ptrs[static_cast<size_t>(s) * km + i])) return fail("stripe pointers mix device and host memory");
@@ -2172,7 +2165,7 @@ class FlagWaits {
     int from = 0;
     if (reached_all(flags, wants, n, from)) return true;
     Record *rec = n <= kMaxFlags ? my_record() : nullptr;
-    if (spin_only_ || !rec) {  // LSEC_WAIT=spin (A/B runs), or no record: spin, then yield, then nap
+    if (!rec) {  // no record: spin, then yield, then nap
       const auto t0 = std::chrono::steady_clock::now();
       for (unsigned i = 0;; ++i) {
         if (reached_all(flags, wants, n, from)) return true;
@@ -2189,7 +2182,7 @@ class FlagWaits {
     const auto t0 = std::chrono::steady_clock::now();
     // spin only while waits are short: under load (waits of 100s of us) a spinner holds a CPU
     // for nothing that the callers' copies need
-    const bool short_waits = !adapt_ || recent_us_.load(std::memory_order_relaxed) < 2 * spin_.count();
+    const bool short_waits = recent_us_.load(std::memory_order_relaxed) < 2 * spin_.count();
     const int active = spinners_.fetch_add(1, std::memory_order_relaxed) + 1;
     if (short_waits && active <= spin_limit_) {
       for (unsigned i = 1;; ++i) {
@@ -2309,18 +2302,13 @@ class FlagWaits {
   }
 
   FlagWaits() {
-    const char *n = getenv("LSEC_WAIT_SPINNERS"), *us = getenv("LSEC_WAIT_SPIN_US"), *np = getenv("LSEC_WAIT_POLLERS");
-    // defaults from tools/gpu_wait_sweep.sh (profiles/r02_v22_wait_sweep.jsonl): a quarter of the
-    // usable CPUs spin, for up to 30 us (an unloaded call completes in 14-20 us)
-    spin_limit_ = n ? std::max(0, atoi(n)) : std::max(1, usable_cpus() / 4);
-    spin_ = std::chrono::microseconds(us ? std::max(0, atoi(us)) : 30);
-    const char *w = getenv("LSEC_WAIT"), *ad = getenv("LSEC_WAIT_ADAPT");
-    spin_only_ = w && strcmp(w, "spin") == 0;
-    adapt_ = !ad || atoi(ad) != 0;
-    // pollers: one per 8 usable CPUs, at most 4 (LSEC_WAIT_POLLERS)
-    npollers_ = np ? std::max(1, std::min(16, atoi(np))) : std::max(1, std::min(4, usable_cpus() / 8));
-    if (!spin_only_)
-      for (int p = 0; p < npollers_; ++p) std::thread([this, p] { poll(p); }).detach();
+    // from a sweep of both (profiles/r02_v22_wait_sweep.jsonl): a quarter of the usable CPUs
+    // spin, for up to 30 us (an unloaded call completes in 14-20 us)
+    spin_limit_ = std::max(1, usable_cpus() / 4);
+    spin_ = std::chrono::microseconds(30);
+    // pollers: one per 8 usable CPUs, at most 4
+    npollers_ = std::max(1, std::min(4, usable_cpus() / 8));
+    for (int p = 0; p < npollers_; ++p) std::thread([this, p] { poll(p); }).detach();
   }
 
   // poller p scans records p, p + npollers, ...: wakes every parked waiter whose flags have all
@@ -2370,8 +2358,6 @@ class FlagWaits {
 
   int spin_limit_ = 1;                   // waiters allowed to spin at once (LSEC_WAIT_SPINNERS)
   std::chrono::microseconds spin_{100};  // how long one spins before parking (LSEC_WAIT_SPIN_US)
-  bool spin_only_ = false;
-  bool adapt_ = true;  // no spinning while recent waits are long (LSEC_WAIT_ADAPT=0: always)
   int npollers_ = 1;
   std::atomic<int> spinners_{0};
   std::atomic<long> recent_us_{0};
@@ -2509,10 +2495,8 @@ class StripeServer {
     const long long unit = kind == KBITSLICED ? 8LL * p->packet_size : 16;
     const long long max_len = direct ? C : static_cast<long long>(kSlotBytes / nio) / unit * unit;
     if (max_len < std::min<long long>(unit, C)) return refuse();
-    static const long long target = [] {  // column bytes per part (LSEC_SRV_PART_KB, A/B runs)
-      const char *v = getenv("LSEC_SRV_PART_KB");
-      return v ? std::max(1LL, atoll(v)) << 10 : 4096LL;
-    }();
+    // column bytes per part: 4 KiB (4-16 KiB parts measured level, profiles/r02_v22_server_part_ab.jsonl)
+    constexpr long long target = 4096;
     long long len = std::min(std::max<long long>(unit, target / unit * unit), max_len);
     if ((C + len - 1) / len > kMaxParts) {
       len = ((C + kMaxParts - 1) / kMaxParts + unit - 1) / unit * unit;
@@ -2926,16 +2910,6 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
   return 0;
 }
 
-// which route serves a host-memory call (LSEC_SMALL_PATH: zerocopy | dispatch; default
-// zerocopy up to zerocopy_limit(), the dispatcher up to coalesce_limit(), then run_host)
-bool zerocopy_enabled() {
-  static const bool on = [] {
-    const char *s = getenv("LSEC_SMALL_PATH");
-    return !s || strcmp(s, "dispatch") != 0;
-  }();
-  return on;
-}
-
 // host-memory batches: small ones are served zero-copy by the calling thread (or coalesced
 // with concurrent callers), large ones stream through their own staging pipeline
 //
@@ -2949,7 +2923,7 @@ bool zerocopy_enabled() {
 int run_host_auto(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
                   const std::vector<int> &out_ids, const void *image, int kind) {
   const size_t bytes = static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()) * C;
-  if (zerocopy_enabled() && bytes <= zerocopy_limit()) {
+  if (bytes <= zerocopy_limit()) {
     const int rc = run_zerocopy(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
     if (rc != 1) return rc;  // 1: its slot would pass the page-locked budget
   }

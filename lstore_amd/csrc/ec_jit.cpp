@@ -87,11 +87,9 @@ bool wants_gfw_net(int R, int K, int w) {
 
 bool wants_xornet(int R, int K) {
   const bool on = jit_on();
-  static const int min_cells = [] {  // LSEC_JIT_MIN: smallest R * K served by a network (A/B runs)
-    const char *s = getenv("LSEC_JIT_MIN");
-    return s ? atoi(s) : 96;
-  }();
-  return on && R >= 2 && R <= kMaxRows && K >= 2 && K <= kMaxCols && R * K >= min_cells;
+  // R * K >= 96 only: narrower codes are memory-bound on the table kernel already (RS(16+4) /
+  // RS(12+4) level within noise on a network, profiles/r02_v15_jit_ab.txt)
+  return on && R >= 2 && R <= kMaxRows && K >= 2 && K <= kMaxCols && R * K >= 96;
 }
 
 // Code shape knobs (LSEC_JIT_VARIANT, read once; A/B runs): bit 0 = common-pair elimination,

@@ -13,12 +13,8 @@ int g_bw_variant = 0, g_bs_variant = 0;
 
 int default_grid(uint64_t ntiles) {
   // One tile per block: on this streaming pattern a full grid beat every grid-stride
-  // size from 2 to 16 blocks per CU by 5-7% (tools/kprobe.hip).  LSEC_GRID_CAP overrides.
-  static const uint64_t cap = [] {
-    const char *s = getenv("LSEC_GRID_CAP");
-    return s ? std::max<uint64_t>(1, strtoull(s, nullptr, 10)) : (1ull << 31) - 1;
-  }();
-  return static_cast<int>(std::min<uint64_t>(std::max<uint64_t>(ntiles, 1), cap));
+  // size from 2 to 16 blocks per CU by 5-7% (tools/kprobe.hip).
+  return static_cast<int>(std::min<uint64_t>(std::max<uint64_t>(ntiles, 1), (1ull << 31) - 1));
 }
 
 template <typename F>
@@ -353,11 +349,8 @@ hipError_t launch_signal(unsigned *counter, unsigned *flag, unsigned value, hipS
 
 hipError_t launch_copy_pieces(const CopyPiece *list, int n, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  static const int grid_cap = [] {  // LSEC_COPY_GRID: A/B runs of the transport's footprint
-    const char *s = getenv("LSEC_COPY_GRID");
-    return s ? std::max(1, atoi(s)) : kCopyGrid;
-  }();
-  hipLaunchKernelGGL(k_copy_pieces, dim3(std::min(n, grid_cap)), dim3(kBlock), 0, st, list, n);
+  // the grid does not matter from 64 to 4096 blocks (profiles/r01_v28_kcopy_grid.txt)
+  hipLaunchKernelGGL(k_copy_pieces, dim3(std::min(n, kCopyGrid)), dim3(kBlock), 0, st, list, n);
   return hipGetLastError();
 }
 

@@ -240,13 +240,12 @@ static void run(int T, const char *impl, const char *method)
     double sum = 0;
     for (long i = 0; i < n; i++) sum += lat[i];
     pthread_barrier_destroy(&g_bar);
-    const char *sp = getenv("LSEC_SMALL_PATH");
     printf("{\"impl\": \"%s\", \"op\": \"%s\", \"chunk\": %d, \"threads\": %d, \"calls\": %ld, \"seconds\": %.3f, "
-           "\"method\": \"%s\", \"pinned\": %d, \"small_path\": \"%s\", \"per_call_us_p50\": %.1f, "
+           "\"method\": \"%s\", \"pinned\": %d, \"per_call_us_p50\": %.1f, "
            "\"per_call_us_p99\": %.1f, \"per_call_us_p999\": %.1f, \"per_call_us_max\": %.1f, \"per_call_us_mean\": %.1f, "
            "\"gibps\": %.3f, \"cpu_util\": %.2f, \"cpu_us_per_call\": %.1f, \"cgroup_throttled_ms\": %.1f, "
            "\"verified\": %ld, \"mismatches\": %ld, \"stripes_per_thread\": %ld, \"set_mib\": %.0f}\n",
-           impl, g_decode ? "decode" : "encode", g_chunk, T, calls, wall, method, g_host_malloc != NULL, sp ? sp : "default",
+           impl, g_decode ? "decode" : "encode", g_chunk, T, calls, wall, method, g_host_malloc != NULL,
            n ? lat[n / 2] * 1e6 : 0.0, n ? lat[(size_t)(n * 0.99)] * 1e6 : 0.0, n ? lat[(size_t)(n * 0.999)] * 1e6 : 0.0,
            n ? lat[n - 1] * 1e6 : 0.0, n ? sum / n * 1e6 : 0.0, calls * (double)g_k * g_chunk / wall / (1 << 30),
            cpu / wall, calls ? cpu / calls * 1e6 : 0.0, thr * 1e3, g_verified, g_mismatch, g_nbuf,
