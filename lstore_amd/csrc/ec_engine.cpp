@@ -1105,8 +1105,10 @@ class InPlacePin {
   ~InPlacePin() { release(); }
   // kernel_ok: the caller can move small runs by kernel (lsec::launch_copy_pieces), so runs
   // below kMinRun are worth pinning too; small_runs() then tells it to do so
+  // all = true (run_registered): pin whatever the size and runs, every region with a device
+  // alias, for a kernel that reads and writes the caller's chunks in place
   bool pin(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
-           long long C, bool kernel_ok) {
+           long long C, bool kernel_ok, bool all = false) {
     static const bool off = getenv("LSEC_NO_HOST_REGISTER") != nullptr;
     if (off) return false;
     std::vector<std::pair<char *, char *>> pieces;
@@ -1127,7 +1129,7 @@ class InPlacePin {
     }
     size_t total = 0;
     for (const auto &r : regions) total += static_cast<size_t>(r.second - r.first);
-    if (total < kMinBytes) return false;  // packing a small batch is cheaper than the syscalls
+    if (total < kMinBytes && !all) return false;  // packing a small batch is cheaper than the syscalls
     // Each DMA from registered pageable memory has a fixed cost on top of the bytes, so pin
     // only when the copies the pinned path will issue (one per run of host-contiguous chunks,
     // stripe by stripe) average >= 2.5 MiB; smaller runs pack faster.  Round 1's 4 MiB had
@@ -1148,7 +1150,7 @@ class InPlacePin {
         }
     }
     if (runs == 0) return false;
-    small_runs_ = total / runs < min_run();
+    small_runs_ = all || total / runs < min_run();
     if (small_runs_ && !kernel_ok) return false;
     {
       // claim the page-rounded regions, so a concurrent call over the same pages packs
@@ -1372,7 +1374,7 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
     if (cb < align) cb = align;
     if (cb >= C) cb = C;
   }
-  int nb_max = cb < C ? 1 : static_cast<int>(std::max<size_t>(1, std::min<size_t>(nstripes, budget / 2 / (per_col * C))));
+  const int nb_max = cb < C ? 1 : static_cast<int>(std::max<size_t>(1, std::min<size_t>(nstripes, budget / 2 / (per_col * C))));
   Staging *stg = acquire_staging(dev);
   if (!stg) return fail("cannot create staging streams");
   int rc = 0;
@@ -1422,27 +1424,6 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   // (profiles/r01_v28_host_trace.txt), but DMA of the same small registered runs is slower still:
   // kernel in + DMA out gave 17-30 GiB/s encode against 28-32 (profiles/r01_v28_kcopy_modes.txt).
   const bool out_by_kernel = by_kernel;
-  // A packed call that fits one staging batch would pack, copy in, compute, copy out and unpack
-  // one after the other.  From 2 MiB such calls are cut into 2-8 batches (of stripes, or of
-  // column blocks of a single stripe), so the copy pool packs batch b+1 while batch b is on PCIe.
-  static const int max_blocks = [] {  // LSEC_HOST_BLOCKS (A/B runs; 1 = one batch)
-    const char *v = getenv("LSEC_HOST_BLOCKS");
-    return v ? std::max(1, atoi(v)) : 8;
-  }();
-  if (!pinned && nb_max >= nstripes && cb == C) {
-    const int nblk = static_cast<int>(std::min<size_t>(max_blocks, (per_col * C * nstripes) >> 20));
-    if (nblk >= 2 && nstripes >= nblk) {
-      nb_max = (nstripes + nblk - 1) / nblk;
-    } else if (nblk >= 2) {
-      const long long per_stripe = (nblk + nstripes - 1) / nstripes;
-      const long long align = packet_kind(kind) ? static_cast<long long>(p->w) * p->packet_size : 8192;
-      const long long c = ((C + per_stripe - 1) / per_stripe + align - 1) / align * align;
-      if (c < C) {
-        cb = c;
-        nb_max = 1;
-      }
-    }
-  }
   const size_t slot_bytes = per_col * static_cast<size_t>(cb) * nb_max;
   const auto t_loop0 = now();
   std::vector<DmaRun> runs;
@@ -2831,6 +2812,43 @@ bool server_enabled() {
   return on;
 }
 
+ZcSlot &thread_zc_slot(int dev);
+
+// Calls of a few large stripes from pageable memory (LStore's 1 MiB chunks: 7-9 MiB per RS(6+3)
+// call), few at a time: register the caller's chunks in place and let one coding kernel read and
+// write them over PCIe through their device aliases -- no host copies, no DMA, one launch.  0
+// served, -1 error, 1 not servable here (the caller takes another route).
+int run_registered(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
+                   const std::vector<int> &out_ids, const void *image, int kind) {
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  hipStream_t st = thread_stream();
+  if (!st) return fail("no HIP stream");
+  const lio_erasure_plan_t *p = &e->pub;
+  const int km = p->data_strips + p->parity_strips;
+  const size_t nin = in_ids.size(), nout = out_ids.size(), nio = nin + nout;
+  ZcSlot &slot = thread_zc_slot(dev);
+  if (slot.init_signal()) return -1;
+  InPlacePin pin;
+  if (!pin.pin(ptrs, nstripes, km, in_ids, out_ids, C, true, true)) return 1;
+  std::vector<uint64_t> a(static_cast<size_t>(nstripes) * nio);
+  for (int s = 0; s < nstripes; ++s)
+    for (size_t i = 0; i < nio; ++i) {
+      const uint64_t d = pin.alias(ptrs[static_cast<size_t>(s) * km + (i < nin ? in_ids[i] : out_ids[i - nin])]);
+      if (!d) return 1;
+      a[static_cast<size_t>(s) * nio + i] = d;
+    }
+  std::vector<int64_t> stride;
+  if (!regular_refs(a, nstripes, nio, stride)) return 1;
+  ShardRef in[kMaxDevs], out[kMaxDevs];
+  for (size_t j = 0; j < nin; ++j) in[j] = {a[j], stride[j]};
+  for (size_t r = 0; r < nout; ++r) out[r] = {a[nin + r], stride[nin + r]};
+  ZcStats::get().launch_direct.fetch_add(1, std::memory_order_relaxed);
+  if (enqueue_apply(kind, image, static_cast<int>(nin), static_cast<int>(nout), in, out, nstripes, C, p->packet_size, st, p->w))
+    return -1;
+  return zc_complete(slot, st);  // every access to the registered pages is done before pin releases them
+}
+
 int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
                  const std::vector<int> &out_ids, const void *image, int kind) {
   if (ZcStats::on()) {
@@ -2846,9 +2864,7 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
   const size_t nin = in_ids.size(), nout = out_ids.size(), nio = nin + nout;
   ShardRef in[kMaxDevs], out[kMaxDevs];
   const bool aligned = kernel_transport_aligned(ptrs, nstripes, km, in_ids, out_ids, C, C);
-  static thread_local std::map<int, std::unique_ptr<ZcSlot>> slots;
-  std::unique_ptr<ZcSlot> &slot = slots[dev];
-  if (!slot) slot.reset(new ZcSlot());
+  ZcSlot *slot = &thread_zc_slot(dev);
   if (slot->init_signal()) return -1;
   CallerPinned cp = caller_pinned(ptrs, nstripes, km, in_ids, out_ids, C, aligned);
   if (nstripes == 1 && server_enabled()) {
@@ -2910,6 +2926,13 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
   return 0;
 }
 
+ZcSlot &thread_zc_slot(int dev) {
+  static thread_local std::map<int, std::unique_ptr<ZcSlot>> slots;
+  std::unique_ptr<ZcSlot> &slot = slots[dev];
+  if (!slot) slot.reset(new ZcSlot());
+  return *slot;
+}
+
 // host-memory batches: small ones are served zero-copy by the calling thread (or coalesced
 // with concurrent callers), large ones stream through their own staging pipeline
 //
@@ -2923,16 +2946,42 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
 int run_host_auto(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
                   const std::vector<int> &out_ids, const void *image, int kind) {
   const size_t bytes = static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()) * C;
+  static const int own_max = [] {  // LSEC_OWN_PIPELINE_MAX: A/B runs (0: always the dispatcher)
+    const char *v = getenv("LSEC_OWN_PIPELINE_MAX");
+    return v ? std::max(0, atoi(v)) : std::max(2, usable_cpus() / 2);
+  }();
+  static std::atomic<int> own_inflight{0};
+  static const bool reg = [] {  // LSEC_REG_ZC=0: no registered zero-copy
+    const char *v = getenv("LSEC_REG_ZC");
+    return !v || *v != '0';
+  }();
+  // Registered zero-copy (run_registered) for calls of 4-16 MiB while at most own_max run, and
+  // from 512 KiB while this call runs alone or with one other: per-stripe 1 MiB Cauchy(6+3)
+  // decodes at one thread 14 -> 38 GiB/s, at 8 threads 27 -> 43; 512 KiB decodes at one thread
+  // 16 -> 33.  Under load the registrations contend in the runtime, and calls below 4 MiB are
+  // faster on the server or their own zero-copy slot (512 KiB decodes at 8 threads 49 vs 37
+  // registered; profiles/r03_v7_route_sweep.jsonl).
+  struct Count {
+    std::atomic<int> &n;
+    const int at;
+    explicit Count(std::atomic<int> &c) : n(c), at(c.fetch_add(1, std::memory_order_acq_rel) + 1) {}
+    ~Count() { n.fetch_sub(1, std::memory_order_acq_rel); }
+  };
+  static std::atomic<int> host_inflight{0};
+  const Count calls(host_inflight);
+  const bool big = bytes >= (4u << 20), alone = calls.at <= 2 && bytes >= (512u << 10);
+  if (reg && (big || alone) && bytes <= coalesce_limit() && own_max > 0) {
+    int rc = 1;
+    if (own_inflight.fetch_add(1, std::memory_order_acq_rel) < own_max)
+      rc = run_registered(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
+    own_inflight.fetch_sub(1, std::memory_order_acq_rel);
+    if (rc != 1) return rc;
+  }
   if (bytes <= zerocopy_limit()) {
     const int rc = run_zerocopy(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
     if (rc != 1) return rc;  // 1: its slot would pass the page-locked budget
   }
   if (bytes <= coalesce_limit()) {
-    static std::atomic<int> own_inflight{0};
-    static const int own_max = [] {  // LSEC_OWN_PIPELINE_MAX: A/B runs (0: always the dispatcher)
-      const char *v = getenv("LSEC_OWN_PIPELINE_MAX");
-      return v ? std::max(0, atoi(v)) : std::max(2, usable_cpus() / 2);
-    }();
     if (bytes >= (4u << 20) && own_max > 0) {
       if (own_inflight.fetch_add(1, std::memory_order_acq_rel) < own_max) {
         const int rc = run_host(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
