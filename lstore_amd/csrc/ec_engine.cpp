@@ -1171,9 +1171,13 @@ class InPlacePin {
         }
       g_inplace.insert(g_inplace.end(), claimed_.begin(), claimed_.end());
     }
+    static const unsigned reg_flags = [] {  // LSEC_REG_FLAGS: extra hipHostRegister flags (A/B runs)
+      const char *v = getenv("LSEC_REG_FLAGS");
+      return v ? static_cast<unsigned>(strtoul(v, nullptr, 0)) : 0u;
+    }();
     for (const auto &r : regions) {
-      if (hipHostRegister(r.first, static_cast<size_t>(r.second - r.first), hipHostRegisterPortable | hipHostRegisterMapped) !=
-          hipSuccess) {
+      if (hipHostRegister(r.first, static_cast<size_t>(r.second - r.first),
+                          hipHostRegisterPortable | hipHostRegisterMapped | (all ? reg_flags : 0u)) != hipSuccess) {
         (void)hipGetLastError();
         release();
         return false;
@@ -2844,6 +2848,14 @@ int run_registered(PlanExt *e, char **ptrs, int nstripes, long long C, const std
   for (size_t j = 0; j < nin; ++j) in[j] = {a[j], stride[j]};
   for (size_t r = 0; r < nout; ++r) out[r] = {a[nin + r], stride[nin + r]};
   ZcStats::get().launch_direct.fetch_add(1, std::memory_order_relaxed);
+  static const bool inv = [] {  // LSEC_REG_INV=0: no L2 invalidation first (A/B runs)
+    const char *v = getenv("LSEC_REG_INV");
+    return !v || *v != '0';
+  }();
+  if (inv) {
+    const hipError_t err = lsec::launch_acquire_system(st);
+    if (err != hipSuccess) return fail("acquire launch: %s", hipGetErrorString(err));
+  }
   if (enqueue_apply(kind, image, static_cast<int>(nin), static_cast<int>(nout), in, out, nstripes, C, p->packet_size, st, p->w))
     return -1;
   return zc_complete(slot, st);  // every access to the registered pages is done before pin releases them
@@ -2910,19 +2922,40 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
     g_zc_slot_bytes.fetch_add(cap, std::memory_order_relaxed);
   }
   ZcStats::get().launch_slot.fetch_add(1, std::memory_order_relaxed);
-  // slot layout: inputs [s][nin][C], then outputs [s][nout][C]
+  // slot layout: inputs [s][nin][C], then outputs [s][nout][C].  Calls of 1 MiB and more are
+  // packed and computed in blocks of about 1 MiB (groups of stripes, or column blocks of a
+  // single stripe): the copy pool packs block b+1 while the kernel of block b reads the slot over
+  // PCIe, and a 7 MiB call no longer waits for all its packing before the GPU starts.
   const size_t in_bytes = static_cast<size_t>(nstripes) * nin * C;
-  for (int s = 0; s < nstripes; ++s)
-    for (size_t j = 0; j < nin; ++j)
-      std::memcpy(slot->h + (s * nin + j) * C, ptrs[static_cast<size_t>(s) * km + in_ids[j]], C);
-  for (size_t j = 0; j < nin; ++j) in[j] = {slot->d + j * C, static_cast<int64_t>(nin * C)};
-  for (size_t r = 0; r < nout; ++r) out[r] = {slot->d + in_bytes + r * C, static_cast<int64_t>(nout * C)};
-  if (enqueue_apply(kind, image, static_cast<int>(nin), static_cast<int>(nout), in, out, nstripes, C, p->packet_size, st, p->w))
-    return -1;
+  const int nblk = static_cast<int>(std::min<size_t>(16, std::max<size_t>(1, need >> 20)));
+  const long long unit = packet_kind(kind) ? static_cast<long long>(p->w) * p->packet_size : 16;
+  const bool by_cols = nstripes == 1 && nblk > 1 && C > unit;
+  const int sg = by_cols ? 1 : (nstripes + nblk - 1) / nblk;                       // stripes per block
+  const long long cl = by_cols ? ((C + nblk - 1) / nblk + unit - 1) / unit * unit : C;  // columns per block
+  std::vector<CopyJob> jobs;
+  for (int s0 = 0; s0 < nstripes; s0 += sg) {
+    const int n = std::min(sg, nstripes - s0);
+    for (long long c0 = 0; c0 < C; c0 += cl) {
+      const long long len = std::min(cl, C - c0);
+      jobs.clear();
+      for (int s = s0; s < s0 + n; ++s)
+        for (size_t j = 0; j < nin; ++j)
+          jobs.push_back({slot->h + (s * nin + j) * C + c0, ptrs[static_cast<size_t>(s) * km + in_ids[j]] + c0,
+                          static_cast<size_t>(len)});
+      CopyPool::get().run(jobs);
+      for (size_t j = 0; j < nin; ++j) in[j] = {slot->d + (s0 * nin + j) * C + c0, static_cast<int64_t>(nin * C)};
+      for (size_t r = 0; r < nout; ++r)
+        out[r] = {slot->d + in_bytes + (s0 * nout + r) * C + c0, static_cast<int64_t>(nout * C)};
+      if (enqueue_apply(kind, image, static_cast<int>(nin), static_cast<int>(nout), in, out, n, len, p->packet_size, st, p->w))
+        return -1;
+    }
+  }
   if (zc_complete(*slot, st)) return -1;
+  jobs.clear();
   for (int s = 0; s < nstripes; ++s)
     for (size_t r = 0; r < nout; ++r)
-      std::memcpy(ptrs[static_cast<size_t>(s) * km + out_ids[r]], slot->h + in_bytes + (s * nout + r) * C, C);
+      jobs.push_back({ptrs[static_cast<size_t>(s) * km + out_ids[r]], slot->h + in_bytes + (s * nout + r) * C, static_cast<size_t>(C)});
+  CopyPool::get().run(jobs);
   return 0;
 }
 
@@ -2951,9 +2984,9 @@ int run_host_auto(PlanExt *e, char **ptrs, int nstripes, long long C, const std:
     return v ? std::max(0, atoi(v)) : std::max(2, usable_cpus() / 2);
   }();
   static std::atomic<int> own_inflight{0};
-  static const bool reg = [] {  // LSEC_REG_ZC=0: no registered zero-copy
+  static const bool reg = [] {  // LSEC_REG_ZC=1: registered zero-copy (experimental, see run_registered)
     const char *v = getenv("LSEC_REG_ZC");
-    return !v || *v != '0';
+    return v && *v == '1';
   }();
   // Registered zero-copy (run_registered) for calls of 4-16 MiB while at most own_max run, and
   // from 512 KiB while this call runs alone or with one other: per-stripe 1 MiB Cauchy(6+3)
@@ -2984,7 +3017,12 @@ int run_host_auto(PlanExt *e, char **ptrs, int nstripes, long long C, const std:
   if (bytes <= coalesce_limit()) {
     if (bytes >= (4u << 20) && own_max > 0) {
       if (own_inflight.fetch_add(1, std::memory_order_acq_rel) < own_max) {
-        const int rc = run_host(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
+        static const bool zc_big = [] {  // LSEC_ZC_BIG=0: 4-16 MiB calls on their own staging pipeline (A/B runs)
+          const char *v = getenv("LSEC_ZC_BIG");
+          return !v || *v != '0';
+        }();
+        int rc = zc_big ? run_zerocopy(e, ptrs, nstripes, C, in_ids, out_ids, image, kind) : 1;
+        if (rc == 1) rc = run_host(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
         own_inflight.fetch_sub(1, std::memory_order_acq_rel);
         return rc;
       }

@@ -15,6 +15,19 @@ from patterns import affine, stripe
 
 pytestmark = pytest.mark.gpu
 
+
+def assert_same(got, want):
+    """bit-exact, or a message locating the differing bytes (stripe, shard, byte offsets)"""
+    if np.array_equal(got, want):
+        return
+    d = np.argwhere(got != want)
+    where = {}
+    for idx in d:
+        where.setdefault(tuple(int(x) for x in idx[:-1]), []).append(int(idx[-1]))
+    msg = "; ".join(f"{k}: {len(v)} bytes in [{min(v)}, {max(v)}] got {got[k][min(v)]} want {want[k][min(v)]}"
+                    for k, v in list(where.items())[:8])
+    raise AssertionError(f"{len(d)} bytes differ: {msg}")
+
 GPU_METHODS = (L.REED_SOL_VAN, L.REED_SOL_R6_OP, L.CAUCHY_ORIG, L.CAUCHY_GOOD, L.RAID4, L.LIBERATION, L.BLAUM_ROTH,
                L.LIBER8TION)
 
@@ -384,7 +397,7 @@ def test_xor_network_vs_oracle(cuda, k, m, size):
         full = host.copy()
         host[:, lost] = 0x33
         p.decode_stripes(host, lost)
-        assert np.array_equal(host, full)
+        assert_same(host, full)
 
 
 @pytest.mark.parametrize("method,k,m,w,size,lost", [
@@ -425,7 +438,7 @@ def test_gfw_network_vs_oracle(cuda, method, k, m, w, size, lost):
         full = host.copy()
         host[:, lost] = 0x33
         p.decode_stripes(host, lost)
-        assert np.array_equal(host, full)
+        assert_same(host, full)
 
 
 def test_stripe_width_limits_are_errors(cuda):
