@@ -743,9 +743,8 @@ class CopyPool {
     return *p;
   }
 
-  void run(std::vector<CopyJob> &jobs) {
-    // split into pieces so every worker gets a share of large chunks
-    constexpr size_t kPiece = 512 << 10;
+  // piece: bytes per work item (every worker gets a share of large chunks)
+  void run(std::vector<CopyJob> &jobs, size_t kPiece = 512 << 10) {
     std::vector<CopyJob> pieces;
     pieces.reserve(jobs.size());
     for (const CopyJob &j : jobs)
@@ -2942,7 +2941,7 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
         for (size_t j = 0; j < nin; ++j)
           jobs.push_back({slot->h + (s * nin + j) * C + c0, ptrs[static_cast<size_t>(s) * km + in_ids[j]] + c0,
                           static_cast<size_t>(len)});
-      CopyPool::get().run(jobs);
+      CopyPool::get().run(jobs, 64 << 10);
       for (size_t j = 0; j < nin; ++j) in[j] = {slot->d + (s0 * nin + j) * C + c0, static_cast<int64_t>(nin * C)};
       for (size_t r = 0; r < nout; ++r)
         out[r] = {slot->d + in_bytes + (s0 * nout + r) * C + c0, static_cast<int64_t>(nout * C)};
@@ -2955,7 +2954,7 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
   for (int s = 0; s < nstripes; ++s)
     for (size_t r = 0; r < nout; ++r)
       jobs.push_back({ptrs[static_cast<size_t>(s) * km + out_ids[r]], slot->h + in_bytes + (s * nout + r) * C, static_cast<size_t>(C)});
-  CopyPool::get().run(jobs);
+  CopyPool::get().run(jobs, 64 << 10);
   return 0;
 }
 
