@@ -30,11 +30,15 @@ def main():
     ap.add_argument("--w", type=int, default=8)
     ap.add_argument("--fresh-plan", action="store_true", help="a new plan (new device images) every iteration")
     ap.add_argument("--dev-first", action="store_true", help="a device-resident encode before the host calls")
+    ap.add_argument("--offset", type=int, default=-1,
+                    help="stripes start this many bytes past a page boundary (-1: wherever numpy puts them)")
+    ap.add_argument("--method", default="reed_sol_van")
     a = ap.parse_args()
     if a.dev_first:
         import torch
         torch.zeros(1, device="cuda")  # torch's HIP runtime first, as in the tests and bench.py
     k, m, C, n = a.k, a.m, a.chunk, a.stripes
+    meth = getattr(L, a.method.upper())
     rng = np.random.default_rng(1)
     bad_enc = bad_dec = 0
     first = None
@@ -43,8 +47,11 @@ def main():
         lost = [0, 3, 5, 9][:m]
 
     def new_plan():
-        p = L.Plan.new(L.REED_SOL_VAN, C, k, m, a.w, 8, 8)
-        assert p.form_encoding_matrix() == 0 and p.form_decoding_matrix() == 0
+        if a.method == "reed_sol_van":
+            p = L.Plan.new(meth, C, k, m, a.w, 8, 8)
+            assert p.form_encoding_matrix() == 0 and p.form_decoding_matrix() == 0
+        else:
+            p = L.Plan.for_chunk(meth, k, m, C, a.w)
         p.prepare_encode()
         p.prepare_decode(lost)
         return p
@@ -63,10 +70,15 @@ def main():
                 p.encode_dev(d, par)
                 torch.cuda.synchronize()
             if buf is None or not a.reuse:
-                buf = np.empty((n, k + m, C), np.uint8)
+                if a.offset < 0:
+                    buf = np.empty((n, k + m, C), np.uint8)
+                else:  # a page-aligned allocation, viewed a.offset bytes in
+                    raw = np.empty(n * (k + m) * C + a.offset + 8192, np.uint8)
+                    at = (-raw.ctypes.data) % 4096 + a.offset
+                    buf = raw[at:at + n * (k + m) * C].reshape(n, k + m, C)
             buf[:, :k] = rng.integers(0, 256, (n, k, C), dtype=np.uint8)
             buf[:, k:] = 0x5A
-            want = np.stack([O.encode(L.REED_SOL_VAN, buf[s, :k], m, 0, a.w) for s in range(n)])
+            want = np.stack([O.encode(meth, buf[s, :k], m, p.packet_size, a.w) for s in range(n)])
             p.encode_stripes(buf)
             if not np.array_equal(buf[:, k:], want):
                 bad_enc += 1
@@ -82,7 +94,7 @@ def main():
     p.close()
     print(json.dumps({"k": k, "m": m, "w": a.w, "chunk": C, "stripes": n, "iters": a.iters, "reuse": a.reuse,
                       "fresh_plan": a.fresh_plan, "dev_first": a.dev_first, "reg_zc": os.environ.get("LSEC_REG_ZC", ""),
-                      "reg_flags": os.environ.get("LSEC_REG_FLAGS", ""), "bad_encode": bad_enc, "bad_decode": bad_dec,
+                      "reg_flags": os.environ.get("LSEC_REG_FLAGS", ""), "offset": a.offset, "method": a.method, "bad_encode": bad_enc, "bad_decode": bad_dec,
                       "first_bad": first}), flush=True)
 
 
