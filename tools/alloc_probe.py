@@ -65,7 +65,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--json", default="")
-    ap.add_argument("--alloc", default="torch", help="torch | hipmalloc | contig (hipDeviceMallocContiguous)")
+    ap.add_argument("--alloc", default="torch",
+                    help="torch | hipmalloc | contig (hipDeviceMallocContiguous); a comma list alternates per trial")
     a = ap.parse_args()
     meth, k, m, C = CONFIGS[a.config]
     pads = [int(x) for x in a.pads.split(",")]
@@ -75,17 +76,19 @@ def main():
     plan = L.Plan.for_chunk(meth, k, m, C)
     plan.prepare_decode([0])
     out = []
+    allocs = a.alloc.split(",")
     for trial in range(a.trials):
+        alloc = allocs[trial % len(allocs)]
         torch.cuda.empty_cache()
         spacer = torch.empty(((trial * 37) % 11 + 1) << 28, dtype=torch.uint8, device=dev)  # 256 MiB .. 2.75 GiB
         P = max(pads)
         raws = []
-        if a.alloc == "torch":
+        if alloc == "torch":
             dbuf = torch.randint(0, 256, (N * k * (C + P),), dtype=torch.uint8, device=dev)
             pbuf = torch.empty((N * m * (C + P),), dtype=torch.uint8, device=dev)
             rbuf = torch.empty((N * (C + P),), dtype=torch.uint8, device=dev)
         else:
-            fl = 4 if a.alloc == "contig" else -1
+            fl = 4 if alloc == "contig" else -1
             raws = [RawDev(N * n * (C + P), fl) for n in (k, m, 1)]
             dbuf, pbuf, rbuf = (r.tensor() for r in raws)
             g = torch.Generator(device=dev)
@@ -119,7 +122,7 @@ def main():
                 assert torch.equal(r[:: max(1, N // 5), 0], d[:: max(1, N // 5), 0])
         for pad in pads:
             te, td = (sorted(x)[len(x) // 2] for x in res[pad])
-            rec = {"config": a.config, "alloc": a.alloc, "trial": trial, "pad": pad, "data_va_mib": (dbuf.data_ptr() >> 20) & 0xFFFFF,
+            rec = {"config": a.config, "alloc": alloc, "trial": trial, "pad": pad, "data_va_mib": (dbuf.data_ptr() >> 20) & 0xFFFFF,
                    "encode_frac": round((k + m) * C * N / te / 8e9, 4), "decode_frac": round((k + 1) * C * N / td / 8e9, 4)}
             out.append(rec)
             print(json.dumps(rec), flush=True)
