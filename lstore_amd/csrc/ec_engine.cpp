@@ -1102,12 +1102,14 @@ CallerPinned caller_pinned(char **ptrs, int nstripes, int km, const std::vector<
 class InPlacePin {
  public:
   ~InPlacePin() { release(); }
-  // kernel_ok: the caller can move small runs by kernel (lsec::launch_copy_pieces), so runs
-  // below kMinRun are worth pinning too; small_runs() then tells it to do so
-  // all = true (run_registered): pin whatever the size and runs, every region with a device
-  // alias, for a kernel that reads and writes the caller's chunks in place
+  // DMA only: a GPU kernel never reads or writes registered pageable pages.  (Kernels reading
+  // and writing them in place -- a registered zero-copy route and a copy-piece transport for
+  // pageable batches, both opt-in in rounds 1-3 -- returned stale bytes and wrote into pages the
+  // caller had since reused, once host arrays were freed and reallocated between calls;
+  // tools/reg_stress.py --churn, profiles/r03_v16_reg_repro.jsonl.  DMA over the same
+  // registrations stayed exact: r03_v18_churn_default_routes.jsonl.)
   bool pin(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
-           long long C, bool kernel_ok, bool all = false) {
+           long long C) {
     static const bool off = getenv("LSEC_NO_HOST_REGISTER") != nullptr;
     if (off) return false;
     std::vector<std::pair<char *, char *>> pieces;
@@ -1128,7 +1130,7 @@ class InPlacePin {
     }
     size_t total = 0;
     for (const auto &r : regions) total += static_cast<size_t>(r.second - r.first);
-    if (total < kMinBytes && !all) return false;  // packing a small batch is cheaper than the syscalls
+    if (total < kMinBytes) return false;  // packing a small batch is cheaper than the syscalls
     // Each DMA from registered pageable memory has a fixed cost on top of the bytes, so pin
     // only when the copies the pinned path will issue (one per run of host-contiguous chunks,
     // stripe by stripe) average >= 2.5 MiB; smaller runs pack faster.  Round 1's 4 MiB had
@@ -1149,8 +1151,7 @@ class InPlacePin {
         }
     }
     if (runs == 0) return false;
-    small_runs_ = all || total / runs < min_run();
-    if (small_runs_ && !kernel_ok) return false;
+    if (total / runs < min_run()) return false;
     {
       // claim the page-rounded regions, so a concurrent call over the same pages packs
       std::lock_guard<std::mutex> lk(g_inplace_mu);
@@ -1170,41 +1171,27 @@ class InPlacePin {
         }
       g_inplace.insert(g_inplace.end(), claimed_.begin(), claimed_.end());
     }
-    static const unsigned reg_flags = [] {  // LSEC_REG_FLAGS: extra hipHostRegister flags (A/B runs)
-      const char *v = getenv("LSEC_REG_FLAGS");
-      return v ? static_cast<unsigned>(strtoul(v, nullptr, 0)) : 0u;
-    }();
+    // whole pages (the claims above are page-rounded and disjoint)
     for (const auto &r : regions) {
-      if (hipHostRegister(r.first, static_cast<size_t>(r.second - r.first),
-                          hipHostRegisterPortable | hipHostRegisterMapped | (all ? reg_flags : 0u)) != hipSuccess) {
+      char *lo = reinterpret_cast<char *>(reinterpret_cast<uintptr_t>(r.first) & ~(kPage - 1));
+      char *hi = reinterpret_cast<char *>((reinterpret_cast<uintptr_t>(r.second) + kPage - 1) & ~(kPage - 1));
+      if (hipHostRegister(lo, static_cast<size_t>(hi - lo), hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
         (void)hipGetLastError();
         release();
         return false;
       }
-      held_.push_back(r.first);
-      void *d = nullptr;
-      if (small_runs_ && (hipHostGetDevicePointer(&d, r.first, 0) != hipSuccess || !d)) {
-        (void)hipGetLastError();
-        release();
-        return false;
-      }
-      alias_.push_back({r.first, r.second, reinterpret_cast<intptr_t>(d) - reinterpret_cast<intptr_t>(r.first)});
+      held_.push_back(lo);
     }
     return true;
   }
-  bool small_runs() const { return !held_.empty() && small_runs_; }
-  // device address of host byte p inside a pinned region (regions are sorted and disjoint)
-  uint64_t alias(const char *p) const {
-    auto it = std::upper_bound(alias_.begin(), alias_.end(), p,
-                               [](const char *q, const Alias &a) { return q < a.lo; });
-    if (it == alias_.begin()) return 0;
-    --it;
-    return p < it->hi ? static_cast<uint64_t>(reinterpret_cast<intptr_t>(p) + it->delta) : 0;
-  }
   void release() {
-    for (char *b : held_) (void)hipHostUnregister(b);
+    for (char *b : held_)
+      if (hipHostUnregister(b) != hipSuccess) {
+        (void)hipGetLastError();
+        static std::atomic<bool> told{false};
+        if (!told.exchange(true)) fprintf(stderr, "liblstore_ec: hipHostUnregister(%p) failed\n", static_cast<void *>(b));
+      }
     held_.clear();
-    alias_.clear();
     if (claimed_.empty()) return;
     std::lock_guard<std::mutex> lk(g_inplace_mu);
     for (const auto &c : claimed_) {
@@ -1223,12 +1210,6 @@ class InPlacePin {
     const char *s = getenv("LSEC_PIN_MIN_RUN_KB");
     return s && *s ? static_cast<size_t>(strtoull(s, nullptr, 10)) << 10 : kMinRun;
   }
-  struct Alias {
-    const char *lo, *hi;
-    intptr_t delta;
-  };
-  bool small_runs_ = false;
-  std::vector<Alias> alias_;
   std::vector<char *> held_;
   std::vector<std::pair<uintptr_t, uintptr_t>> claimed_;
 };
@@ -1262,15 +1243,13 @@ size_t add_pieces(lsec::CopyPiece *pl, size_t n, uint64_t src, uint64_t dst, siz
 //   unset  caller page-locked buffers with small runs move by kernel (DMA of their 384 KiB runs
 //          moves 17-20 GiB/s at C = 64 KiB, the kernel 30 / 38: profiles/r01_v28_kcopy_pinned.txt);
 //          pageable batches with small runs are packed
-//   1      pageable ones too: pinned in place and moved by kernel over their device aliases (it
-//          held 29-32 GiB/s encode / 36-41 decode for C = 64-512 KiB whatever the host cores did,
-//          where packing ran 23-38 / 28-45 depending on them: r01_v27_kernel_copy_ab.txt)
 //   0      never
-enum class KernelCopy { kNever, kCallerPinned, kAll };
+// (Until round 3, `1` also pinned pageable batches in place for the copy kernel; kernels over
+// per-call registrations of pageable pages are gone, see InPlacePin.)
+enum class KernelCopy { kNever, kCallerPinned };
 KernelCopy kernel_copy_policy() {
   const char *on = getenv("LSEC_KERNEL_COPY");
-  if (!on || !*on) return KernelCopy::kCallerPinned;
-  return *on == '1' ? KernelCopy::kAll : *on == '0' ? KernelCopy::kNever : KernelCopy::kCallerPinned;
+  return on && *on == '0' ? KernelCopy::kNever : KernelCopy::kCallerPinned;
 }
 
 // every transferred chunk (and column block) 16-byte aligned, as the copy-piece kernel needs
@@ -1409,20 +1388,18 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   const bool aligned = kpol != KernelCopy::kNever && kernel_transport_aligned(ptrs, nstripes, km, in_ids, out_ids, C, cb);
   CallerPinned cp = caller_pinned(ptrs, nstripes, km, in_ids, out_ids, C, aligned);
   const bool caller_pinned = cp.pinned;
-  const bool pinned =
-      caller_pinned || inplace.pin(ptrs, nstripes, km, in_ids, out_ids, C, aligned && kpol == KernelCopy::kAll);
+  const bool pinned = caller_pinned || inplace.pin(ptrs, nstripes, km, in_ids, out_ids, C);
   const std::vector<uint64_t> &calias = cp.dev;  // caller-pinned chunks moved by kernel: their device addresses
   const bool caller_by_kernel = cp.by_kernel;
   const size_t nio = in_ids.size() + out_ids.size();
   // device address of byte c0 of chunk (stripe s, list position i: inputs, then outputs)
-  const auto dev_at = [&](int s, size_t i, int id, long long c0) -> uint64_t {
-    if (caller_by_kernel) return calias[static_cast<size_t>(s) * nio + i] + static_cast<uint64_t>(c0);
-    return inplace.alias(ptrs[static_cast<size_t>(s) * km + id] + c0);
+  const auto dev_at = [&](int s, size_t i, int, long long c0) -> uint64_t {
+    return calias[static_cast<size_t>(s) * nio + i] + static_cast<uint64_t>(c0);
   };
-  // small host runs pinned in place move by kernel over their device aliases: one launch per
-  // direction instead of a DMA per run (each DMA from registered pageable memory costs ~50 us;
-  // 256 KiB runs move at 18 GB/s by DMA, 54 GB/s by one kernel: profiles/r01_v27_zerocopy_probe.txt)
-  const bool by_kernel = inplace.small_runs() || caller_by_kernel;
+  // small caller page-locked runs move by kernel over their device addresses: one launch per
+  // direction instead of a DMA per run (256 KiB runs move at 18 GB/s by DMA, 54 GB/s by one
+  // kernel: profiles/r01_v27_zerocopy_probe.txt)
+  const bool by_kernel = caller_by_kernel;
   // Outputs go back by kernel too.  GPU-initiated reads and writes of host memory share ~52 GB/s
   // (profiles/r01_v28_host_trace.txt), but DMA of the same small registered runs is slower still:
   // kernel in + DMA out gave 17-30 GiB/s encode against 28-32 (profiles/r01_v28_kcopy_modes.txt).
@@ -2817,49 +2794,6 @@ bool server_enabled() {
 
 ZcSlot &thread_zc_slot(int dev);
 
-// Calls of a few large stripes from pageable memory (LStore's 1 MiB chunks: 7-9 MiB per RS(6+3)
-// call), few at a time: register the caller's chunks in place and let one coding kernel read and
-// write them over PCIe through their device aliases -- no host copies, no DMA, one launch.  0
-// served, -1 error, 1 not servable here (the caller takes another route).
-int run_registered(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
-                   const std::vector<int> &out_ids, const void *image, int kind) {
-  int dev = 0;
-  HIP_OK(hipGetDevice(&dev));
-  hipStream_t st = thread_stream();
-  if (!st) return fail("no HIP stream");
-  const lio_erasure_plan_t *p = &e->pub;
-  const int km = p->data_strips + p->parity_strips;
-  const size_t nin = in_ids.size(), nout = out_ids.size(), nio = nin + nout;
-  ZcSlot &slot = thread_zc_slot(dev);
-  if (slot.init_signal()) return -1;
-  InPlacePin pin;
-  if (!pin.pin(ptrs, nstripes, km, in_ids, out_ids, C, true, true)) return 1;
-  std::vector<uint64_t> a(static_cast<size_t>(nstripes) * nio);
-  for (int s = 0; s < nstripes; ++s)
-    for (size_t i = 0; i < nio; ++i) {
-      const uint64_t d = pin.alias(ptrs[static_cast<size_t>(s) * km + (i < nin ? in_ids[i] : out_ids[i - nin])]);
-      if (!d) return 1;
-      a[static_cast<size_t>(s) * nio + i] = d;
-    }
-  std::vector<int64_t> stride;
-  if (!regular_refs(a, nstripes, nio, stride)) return 1;
-  ShardRef in[kMaxDevs], out[kMaxDevs];
-  for (size_t j = 0; j < nin; ++j) in[j] = {a[j], stride[j]};
-  for (size_t r = 0; r < nout; ++r) out[r] = {a[nin + r], stride[nin + r]};
-  ZcStats::get().launch_direct.fetch_add(1, std::memory_order_relaxed);
-  static const bool inv = [] {  // LSEC_REG_INV=0: no L2 invalidation first (A/B runs)
-    const char *v = getenv("LSEC_REG_INV");
-    return !v || *v != '0';
-  }();
-  if (inv) {
-    const hipError_t err = lsec::launch_acquire_system(st);
-    if (err != hipSuccess) return fail("acquire launch: %s", hipGetErrorString(err));
-  }
-  if (enqueue_apply(kind, image, static_cast<int>(nin), static_cast<int>(nout), in, out, nstripes, C, p->packet_size, st, p->w))
-    return -1;
-  return zc_complete(slot, st);  // every access to the registered pages is done before pin releases them
-}
-
 int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
                  const std::vector<int> &out_ids, const void *image, int kind) {
   if (ZcStats::on()) {
@@ -2983,32 +2917,6 @@ int run_host_auto(PlanExt *e, char **ptrs, int nstripes, long long C, const std:
     return v ? std::max(0, atoi(v)) : std::max(2, usable_cpus() / 2);
   }();
   static std::atomic<int> own_inflight{0};
-  static const bool reg = [] {  // LSEC_REG_ZC=1: registered zero-copy (experimental, see run_registered)
-    const char *v = getenv("LSEC_REG_ZC");
-    return v && *v == '1';
-  }();
-  // Registered zero-copy (run_registered) for calls of 4-16 MiB while at most own_max run, and
-  // from 512 KiB while this call runs alone or with one other: per-stripe 1 MiB Cauchy(6+3)
-  // decodes at one thread 14 -> 38 GiB/s, at 8 threads 27 -> 43; 512 KiB decodes at one thread
-  // 16 -> 33.  Under load the registrations contend in the runtime, and calls below 4 MiB are
-  // faster on the server or their own zero-copy slot (512 KiB decodes at 8 threads 49 vs 37
-  // registered; profiles/r03_v7_route_sweep.jsonl).
-  struct Count {
-    std::atomic<int> &n;
-    const int at;
-    explicit Count(std::atomic<int> &c) : n(c), at(c.fetch_add(1, std::memory_order_acq_rel) + 1) {}
-    ~Count() { n.fetch_sub(1, std::memory_order_acq_rel); }
-  };
-  static std::atomic<int> host_inflight{0};
-  const Count calls(host_inflight);
-  const bool big = bytes >= (4u << 20), alone = calls.at <= 2 && bytes >= (512u << 10);
-  if (reg && (big || alone) && bytes <= coalesce_limit() && own_max > 0) {
-    int rc = 1;
-    if (own_inflight.fetch_add(1, std::memory_order_acq_rel) < own_max)
-      rc = run_registered(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
-    own_inflight.fetch_sub(1, std::memory_order_acq_rel);
-    if (rc != 1) return rc;
-  }
   if (bytes <= zerocopy_limit()) {
     const int rc = run_zerocopy(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
     if (rc != 1) return rc;  // 1: its slot would pass the page-locked budget

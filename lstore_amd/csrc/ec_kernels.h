@@ -138,9 +138,6 @@ hipError_t launch_copy_pieces(const CopyPiece *list, int n, hipStream_t stream);
 // `flag` (page-locked host memory) with system-scope release.  Launched on the call's stream
 // right after its coding kernel, so stream order puts every byte the call wrote before the flag.
 hipError_t launch_signal(unsigned *counter, unsigned *flag, unsigned value, hipStream_t stream);
-// system-scope acquire (L2 invalidation of host-memory lines) on every XCD, before a kernel
-// reads host pages registered for the call
-hipError_t launch_acquire_system(hipStream_t stream);
 
 // HBM probe (measurement only): dst <- src, bytes a multiple of 16, both 16-byte aligned.
 hipError_t launch_hbm_copy(void *dst, const void *src, uint64_t bytes, hipStream_t stream);

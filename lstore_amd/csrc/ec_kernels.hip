@@ -341,17 +341,6 @@ __global__ __launch_bounds__(64) void k_signal(unsigned *counter, unsigned *flag
 
 }  // namespace
 
-// A system-scope acquire on every XCD: drops the L2 lines of host memory that a kernel reading
-// host pages in place must not hit (lines a cached mapping of the same physical pages left
-// behind before the pages were freed and handed to another buffer).  64 blocks, so that every
-// XCD runs several whatever the dispatcher's placement.
-__global__ __launch_bounds__(64) void k_acquire_system() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
-
-hipError_t launch_acquire_system(hipStream_t st) {
-  hipLaunchKernelGGL(k_acquire_system, dim3(64), dim3(64), 0, st);
-  return hipGetLastError();
-}
-
 hipError_t launch_signal(unsigned *counter, unsigned *flag, unsigned value, hipStream_t st) {
   if (!counter || !flag) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_signal, dim3(kSignalBlocks), dim3(64), 0, st, counter, flag, value);

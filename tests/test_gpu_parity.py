@@ -972,23 +972,13 @@ def test_zero_ones_and_single_bit_patterns(cuda, method, k, m, size):
                                                             (L.REED_SOL_VAN, 6, 3, 64 << 10, 200, 0, True),
                                                             (L.CAUCHY_GOOD, 6, 3, 64 << 10, 64, 0, True),
                                                             (L.REED_SOL_VAN, 6, 3, 64 << 10, 40, 8, True)])
-def test_pageable_small_runs_by_kernel(cuda, method, k, m, size, n, shift, pinned):
-    """With LSEC_KERNEL_COPY=1, large pageable batches of small chunks (LStore's [stripe][k+m][C]
-    pages, runs well under 4 MiB) are pinned in place and moved by the copy-piece kernel over
-    their device aliases (by default they pack);
-    8-byte-misaligned buffers (shift=8) cannot be, and pack.  Caller page-locked buffers
-    (pinned=True) with small runs move by kernel by default, after every chunk is checked;
-    misaligned ones DMA.  Encode and a double-erasure decode are bit-exact either way."""
-    import os
-
-    if pinned:                              # caller page-locked: kernel transport by default
-        _small_runs_case(method, k, m, size, n, shift, pinned)
-        return
-    os.environ["LSEC_KERNEL_COPY"] = "1"    # pageable: opt-in, read per call
-    try:
-        _small_runs_case(method, k, m, size, n, shift, pinned)
-    finally:
-        del os.environ["LSEC_KERNEL_COPY"]
+def test_small_run_batches(cuda, method, k, m, size, n, shift, pinned):
+    """Large batches of small chunks (LStore's [stripe][k+m][C] pages, runs well under 4 MiB):
+    pageable ones pack (no kernel ever touches per-call registrations of pageable pages, see
+    InPlacePin); caller page-locked buffers (pinned=True) with small runs move by the copy-piece
+    kernel after every chunk is checked, 8-byte-misaligned ones (shift=8) DMA.  Encode and a
+    double-erasure decode are bit-exact either way."""
+    _small_runs_case(method, k, m, size, n, shift, pinned)
 
 
 def _small_runs_case(method, k, m, size, n, shift, pinned):

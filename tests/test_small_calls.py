@@ -9,6 +9,7 @@ addresses while the server runs.
 import json
 import os
 import subprocess
+import sys
 import threading
 import time
 
@@ -170,3 +171,26 @@ def test_fn_pointer_stress_bit_exact(cuda, chunk, threads, method, op, pinned, e
     assert out.returncode == 0, (out.returncode, out.stdout[-500:], out.stderr[-500:])
     rec = json.loads(out.stdout.strip().splitlines()[-1])
     assert rec["verified"] > 0 and rec["mismatches"] == 0, rec
+
+
+STRESS = os.path.join(ROOT, "tools", "reg_stress.py")
+
+
+@pytest.mark.parametrize("args", [
+    ["--k", "6", "--m", "3", "--w", "16", "--chunk", "49192"],
+    ["--method", "cauchy_good", "--k", "6", "--m", "3", "--chunk", "65536", "--stripes", "1"],
+    ["--k", "6", "--m", "3", "--chunk", "1048576", "--stripes", "4"],
+    ["--method", "cauchy_good", "--k", "6", "--m", "3", "--chunk", "65536", "--stripes", "2", "--pinned"],
+])
+def test_host_calls_under_memory_churn(cuda, args):
+    """Host calls while the process frees and reallocates host memory between them (virtual
+    ranges and physical pages recycled; tools/reg_stress.py --churn), with stripe-server calls in
+    between: the zero-copy slots and server, the in-place-pinned DMA pipeline (36 MiB batches) and
+    caller page-locked buffers reallocated every call.  Every call's bytes are checked against the
+    oracle restatement.  (Kernels over per-call registrations of pageable pages failed exactly this,
+    which is why no route uses them: DESIGN.md §1.)"""
+    out = subprocess.run([sys.executable, STRESS, "--seconds", "5", "--churn", "--small-mix", *args],
+                         capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, (out.stdout[-500:], out.stderr[-800:])
+    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    assert rec["iters"] > 10 and rec["bad_encode"] == 0 and rec["bad_decode"] == 0 and rec["bad_small"] == 0, rec
