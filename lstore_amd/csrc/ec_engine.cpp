@@ -2364,6 +2364,9 @@ struct ZcStats {
   // layout and pinned-memory lookups), claim + copies in + posts, wait, copies out
   std::atomic<unsigned long long> t_setup{0}, t_zc{0}, t_post{0}, t_wait{0}, t_out{0};
   std::atomic<unsigned long long> c_setup{0}, c_zc{0}, c_post{0}, c_wait{0}, c_out{0};  // thread CPU ns
+  // own-slot calls, wall time (ns): slot allocation, packing the inputs, enqueueing the block
+  // kernels, waiting for the last one, copying the outputs back
+  std::atomic<unsigned long long> s_alloc{0}, s_pack{0}, s_enq{0}, s_wait{0}, s_out{0};
   static bool on() {
     static const bool v = getenv("LSEC_STATS") != nullptr;
     return v;
@@ -2387,6 +2390,9 @@ struct ZcStats {
         fprintf(stderr, "[lsec stats] server calls, mean thread CPU us: setup %.2f (of it in run_zerocopy %.2f), claim+copy-in+post "
                 "%.2f, wait %.2f, copy-out %.2f\n", z.c_setup.load() / n, z.c_zc.load() / n, z.c_post.load() / n,
                 z.c_wait.load() / n, z.c_out.load() / n);
+        const double ns = static_cast<double>(std::max(1ULL, z.launch_slot.load())) * 1e3;
+        fprintf(stderr, "[lsec stats] own-slot calls, mean wall us: slot %.2f, pack %.2f, enqueue %.2f, wait %.2f, copy-out %.2f\n",
+                z.s_alloc.load() / ns, z.s_pack.load() / ns, z.s_enq.load() / ns, z.s_wait.load() / ns, z.s_out.load() / ns);
       });
       return p;
     }();
@@ -2855,6 +2861,44 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
     g_zc_slot_bytes.fetch_add(cap, std::memory_order_relaxed);
   }
   ZcStats::get().launch_slot.fetch_add(1, std::memory_order_relaxed);
+  const bool stats = ZcStats::on();
+  const auto tnow = [] { return std::chrono::steady_clock::now(); };
+  const auto tns = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return static_cast<unsigned long long>(std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count());
+  };
+  auto t_last = stats ? tnow() : std::chrono::steady_clock::time_point{};
+  // Packing: a call running alone (with at most one other) copies its own chunks -- one thread
+  // packed a 1 MiB Cauchy(6+3) decode's 6 MiB in 164 us against 200 us on the 8-thread copy pool,
+  // at a quarter of the CPU (profiles/r03_v20_slot_phases.txt; 1 MiB decodes at one thread
+  // 19.1 -> 22.6 GiB/s, RS(6+3) 1 MiB encodes 12.9 -> 16.1).  Under concurrency the pool, whose
+  // workers sit on the GPU's NUMA node, packs faster (8 threads: 46.0 pool vs 34.8 inline;
+  // profiles/r03_v21_fnptr_fair.jsonl).  LSEC_ZC_POOL=1 / 0 forces either (A/B runs).
+  static const int pool_mode = [] {
+    const char *v = getenv("LSEC_ZC_POOL");
+    return v && *v ? (*v == '1' ? 1 : 0) : -1;
+  }();
+  static std::atomic<int> slot_calls{0};
+  struct InFlight {
+    std::atomic<int> &n;
+    const int at;
+    explicit InFlight(std::atomic<int> &c) : n(c), at(c.fetch_add(1, std::memory_order_acq_rel) + 1) {}
+    ~InFlight() { n.fetch_sub(1, std::memory_order_acq_rel); }
+  } inflight(slot_calls);
+  const bool pool = pool_mode >= 0 ? pool_mode == 1 : inflight.at > 2;
+  const auto pack = [&](std::vector<CopyJob> &js) {
+    if (pool) {
+      CopyPool::get().run(js, 64 << 10);
+      return;
+    }
+    for (const CopyJob &j : js) std::memcpy(j.dst, j.src, j.bytes);
+  };
+  if (stats) ZcStats::get().s_alloc.fetch_add(tns(tl_zc_t0, t_last), std::memory_order_relaxed);
+  const auto lap = [&](std::atomic<unsigned long long> &acc) {
+    if (!stats) return;
+    const auto t = tnow();
+    acc.fetch_add(tns(t_last, t), std::memory_order_relaxed);
+    t_last = t;
+  };
   // slot layout: inputs [s][nin][C], then outputs [s][nout][C].  Calls of 1 MiB and more are
   // packed and computed in blocks of about 1 MiB (groups of stripes, or column blocks of a
   // single stripe): the copy pool packs block b+1 while the kernel of block b reads the slot over
@@ -2875,20 +2919,24 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
         for (size_t j = 0; j < nin; ++j)
           jobs.push_back({slot->h + (s * nin + j) * C + c0, ptrs[static_cast<size_t>(s) * km + in_ids[j]] + c0,
                           static_cast<size_t>(len)});
-      CopyPool::get().run(jobs, 64 << 10);
+      pack(jobs);
+      lap(ZcStats::get().s_pack);
       for (size_t j = 0; j < nin; ++j) in[j] = {slot->d + (s0 * nin + j) * C + c0, static_cast<int64_t>(nin * C)};
       for (size_t r = 0; r < nout; ++r)
         out[r] = {slot->d + in_bytes + (s0 * nout + r) * C + c0, static_cast<int64_t>(nout * C)};
       if (enqueue_apply(kind, image, static_cast<int>(nin), static_cast<int>(nout), in, out, n, len, p->packet_size, st, p->w))
         return -1;
+      lap(ZcStats::get().s_enq);
     }
   }
   if (zc_complete(*slot, st)) return -1;
+  lap(ZcStats::get().s_wait);
   jobs.clear();
   for (int s = 0; s < nstripes; ++s)
     for (size_t r = 0; r < nout; ++r)
       jobs.push_back({ptrs[static_cast<size_t>(s) * km + out_ids[r]], slot->h + in_bytes + (s * nout + r) * C, static_cast<size_t>(C)});
-  CopyPool::get().run(jobs, 64 << 10);
+  pack(jobs);
+  lap(ZcStats::get().s_out);
   return 0;
 }
 

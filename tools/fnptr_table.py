@@ -1,31 +1,41 @@
 #!/usr/bin/env python3
-"""Tabulate tools/fnptr_bench.c JSON lines (gpurun_out/fnptr_*.jsonl): per (op, method, chunk,
-threads) the reference, the engine's default small-call path, the dispatcher path and the
-page-locked-caller case, GiB/s of user data and p50 / p99 latency per call."""
+"""Tabulate tools/fnptr_bench.c JSON lines (gpurun_out/fnptr_*.jsonl, e.g. from
+tools/gpu_fnptr_fair.sh): per (op, method, chunk, threads) the reference (oracle/_ref, the real
+Jerasure) and the engine (pageable or page-locked buffers, and any environment the run set), GiB/s
+of user data with p50 / p99 latency per call.  Several lines of one kind are averaged
+(gpu_fnptr_fair.sh times the reference twice per case).
+
+python tools/fnptr_table.py gpurun_out/fnptr_fair_<tag>.jsonl [...]
+"""
 import json
 import sys
 from collections import defaultdict
 
 
+def cell(rs):
+    mean = lambda f: sum(r[f] for r in rs) / len(rs)  # noqa: E731
+    return f"{mean('gibps'):.1f} ({mean('per_call_us_p50'):.0f} / {mean('per_call_us_p99'):.0f})", mean("gibps")
+
+
 def main():
-    g = defaultdict(dict)
+    ref = defaultdict(list)
+    eng = defaultdict(list)
     for path in sys.argv[1:]:
         for line in open(path):
             r = json.loads(line)
             key = (r["op"], r["method"], r["chunk"], r["threads"])
-            kind = "ref" if r["impl"] == "reference" else ("pin" if r["pinned"] else
-                                                          ("disp" if r["small_path"] == "dispatch" else "eng"))
-            g[key][kind] = r
-    cols = [("ref", "reference"), ("eng", "engine"), ("disp", "dispatcher"), ("pin", "engine, page-locked")]
-    print("| op | method | C | threads | " + " | ".join(f"{n} GiB/s (p50 / p99 us)" for _, n in cols) + " |")
-    print("|---" * (4 + len(cols)) + "|")
-    for key in sorted(g):
-        d = g[key]
-        cells = []
-        for k, _ in cols:
-            r = d.get(k)
-            cells.append(f"{r['gibps']:.1f} ({r['per_call_us_p50']:.0f} / {r['per_call_us_p99']:.0f})" if r else "-")
-        print(f"| {key[0]} | {key[1]} | {key[2] >> 10} KiB | {key[3]} | " + " | ".join(cells) + " |")
+            if r["impl"] == "reference":
+                ref[key].append(r)
+            else:
+                env = r.get("env", "").strip()
+                eng[key + (("page-locked " if r["pinned"] else "") + env,)].append(r)
+    print("| op | method | C | threads | engine run | reference GiB/s (p50 / p99 us) | engine GiB/s (p50 / p99 us) | engine / reference |")
+    print("|---|---|---|---|---|---|---|---|")
+    for key in sorted(eng, key=lambda k: (k[0], k[1], k[2], k[3], k[4])):
+        rc, rv = cell(ref[key[:4]]) if ref.get(key[:4]) else ("-", None)
+        ec, ev = cell(eng[key])
+        ratio = f"{ev / rv:.2f}" if rv else "-"
+        print(f"| {key[0]} | {key[1]} | {key[2] >> 10} KiB | {key[3]} | {key[4] or 'default'} | {rc} | {ec} | {ratio} |")
 
 
 if __name__ == "__main__":
