@@ -155,7 +155,10 @@ int lsec_segment_write_iov(lio_erasure_plan_t *plan, const struct iovec *iov, in
 #define LSEC_MAGIC_LEGACY  2   /* segment magic_cksum == 0: magics are not adler32 sums, so
                                   stripes are verified with control chunks (jerasure.c:218-266) */
 #define LSEC_INSPECT_FIX   4   /* inspect: repair in place (INSPECT_{QUICK,SCAN,FULL}_REPAIR) */
-#define LSEC_MAX_DEVS      256
+#define LSEC_MAX_DEVS      256  /* k + m of the segment paths, of w = 8 and of the bitmatrix codes;
+                                  the GF(2^16) / GF(2^32) matrix codes (RS, r6, Cauchy) take up
+                                  to LSEC_MAX_DEVS_WIDE through the et_* / lsec_*_dev calls */
+#define LSEC_MAX_DEVS_WIDE 1024
 
 /* Batched read side for whole stripes (segjerase_read_func, segment/jerasure.c:1255-1631):
  * dev[i] are device images laid out as lsec_segment_write writes them (NULL = device

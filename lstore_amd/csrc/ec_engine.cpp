@@ -74,10 +74,16 @@ int fail(const char *fmt, ...) {
 
 enum KernelKind { KNONE = 0, KBYTEWISE = 1, KBITSLICED = 2, KBITMATRIX = 3, KWORDWISE = 4, KBITSLICEDW = 5 };
 
-// devices per stripe: Jerasure takes k + m <= 2^w (reed_sol.c:247-248, cauchy.c:139), 256 at w = 8;
-// the engine takes k + m <= 256 at every w (LSEC_MAX_DEVS).  Inputs beyond lsec::kMaxK per launch
-// run as several launches over the grouped image layout (ec_kernels.h).
-constexpr int kMaxDevs = LSEC_MAX_DEVS;
+// devices per stripe: Jerasure takes k + m <= 2^w (reed_sol.c:247-248, cauchy.c:139), 256 at w = 8.
+// The engine takes that at w = 8 and for the bitmatrix codes (LSEC_MAX_DEVS), and up to
+// kMaxDevs = 1024 for the GF(2^16) / GF(2^32) matrix codes (RS, r6, Cauchy); the segment adapters
+// keep LSEC_MAX_DEVS, which sizes their ABI structs.  Inputs beyond lsec::kMaxK per launch run as
+// several launches over the grouped image layout (ec_kernels.h).
+constexpr int kMaxDevs = LSEC_MAX_DEVS_WIDE;
+int max_devs(int method, int w) {
+  const bool matrix = method == REED_SOL_VAN || method == REED_SOL_R6_OP || method == CAUCHY_ORIG || method == CAUCHY_GOOD;
+  return matrix && (w == 16 || w == 32) ? kMaxDevs : LSEC_MAX_DEVS;
+}
 
 struct DecodeEntry {
   lsec::gf8::DecodePlan dp;
@@ -583,7 +589,8 @@ int decode_kind(const PlanExt *e, const DecodeEntry *ent) {
 
 int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
   const int k = p->data_strips, m = p->parity_strips;
-  if (k < 1 || m < 1 || k + m > kMaxDevs) return fail("k=%d m=%d: k+m outside 2..%d", k, m, kMaxDevs);
+  const int lim = max_devs(p->method, p->w);
+  if (k < 1 || m < 1 || k + m > lim) return fail("k=%d m=%d: k+m outside 2..%d (w=%d)", k, m, lim, p->w);
   if (block_size < 0 || block_size % 8 != 0) return fail("block_size %lld is not a multiple of 8", block_size);
   const int kind = kernel_kind(p->method, p->w);
   if (kind == KNONE)
@@ -3732,8 +3739,9 @@ lio_erasure_plan_t *et_generate_plan(long long int file_size, int method, int da
     fail("et_generate_plan: %s at w=%d has no GPU kernel in this build", JE_method[method], w);
     return nullptr;
   }
-  if (data_strips < 1 || parity_strips < 1 || data_strips + parity_strips > kMaxDevs) {
-    fail("et_generate_plan: k=%d m=%d: k+m outside the engine's 2..%d", data_strips, parity_strips, kMaxDevs);
+  if (data_strips < 1 || parity_strips < 1 || data_strips + parity_strips > max_devs(method, w)) {
+    fail("et_generate_plan: k=%d m=%d: k+m outside the engine's 2..%d at w=%d", data_strips, parity_strips,
+         max_devs(method, w), w);
     return nullptr;
   }
   if (packet_kind(kind) && best_size != file_size && file_size % data_strips == 0) {

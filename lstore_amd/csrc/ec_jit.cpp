@@ -379,11 +379,10 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
     << "  const unsigned nt = tps * (unsigned)a.nstripes;\n"
        "  const unsigned nb = gridDim.x, per = nb >> 3, rem = nb & 7, xcd = blockIdx.x & 7;\n"
        "  const unsigned t0 = xcd * per + (xcd < rem ? xcd : rem) + (blockIdx.x >> 3);\n"
-    ;
-  // bit 19: no cross-tile prefetch (by default the next tile's first inputs are loaded before this
-  // tile's output transposes and stores, so loads stay in flight across the tile boundary; the
-  // input buffers are free by then, so it costs no registers)
-  const bool xtile = !((jit_variant() >> 19) & 1);
+       "  for (unsigned t = t0; t < nt; t += nb) {\n"
+       "    const unsigned s = t / tps;\n"
+    << "    const long long base = (long long)(t - s * tps) * " << tile << " + threadIdx.x * 16;\n";
+  for (int r = 0; r < R; ++r) s << "    u32 h" << r << "[W];\n";
   std::vector<std::vector<bool>> live(R, std::vector<bool>(W, false));
   // inputs with a non-zero coefficient in some row, each loaded one input ahead of its use: the
   // scheduler would otherwise hoist every input's loads to the top (K x W registers live: spills
@@ -396,34 +395,12 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
         break;
       }
   const size_t nbuf = static_cast<size_t>(ahead) + 1;
-  auto load_at = [&](size_t u, const char *sv, const char *bv) {
+  auto load = [&](size_t u) {
     const int j = used[u];
-    s << "    ld(e" << u % nbuf << ", a.in[" << j << "].base + (unsigned long long)" << sv << " * a.in[" << j << "].stride + "
-      << bv << ");\n";
+    s << "    ld(e" << u % nbuf << ", a.in[" << j << "].base + (unsigned long long)s * a.in[" << j << "].stride + base);\n";
   };
-  auto load = [&](size_t u) { load_at(u, "s", "base"); };
-  const std::string tile_base = "(long long)(T - S * tps) * " + std::to_string(tile) + " + threadIdx.x * 16";
-  auto at = [&](const char *T, const char *S) {
-    std::string b = tile_base;
-    for (size_t i; (i = b.find('T')) != std::string::npos;) b.replace(i, 1, T);
-    for (size_t i; (i = b.find('S')) != std::string::npos;) b.replace(i, 1, S);
-    return b;
-  };
-  const size_t first = std::min(used.size(), static_cast<size_t>(ahead));
-  if (xtile) {  // input buffers live across tiles; the first tile's first inputs before the loop
-    for (size_t b = 0; b < nbuf; ++b) s << "  u32 e" << b << "[W];\n";
-    s << "  if (t0 < nt) {\n    const unsigned s = t0 / tps;\n    const long long base = " << at("t0", "s") << ";\n";
-    for (size_t u = 0; u < first; ++u) load(u);
-    s << "  }\n";
-  }
-  s << "  for (unsigned t = t0; t < nt; t += nb) {\n"
-       "    const unsigned s = t / tps;\n"
-    << "    const long long base = " << at("t", "s") << ";\n";
-  for (int r = 0; r < R; ++r) s << "    u32 h" << r << "[W];\n";
-  if (!xtile) {
-    for (size_t b = 0; b < nbuf; ++b) s << "    u32 e" << b << "[W];\n";
-    for (size_t u = 0; u < first; ++u) load(u);
-  }
+  for (size_t b = 0; b < nbuf; ++b) s << "    u32 e" << b << "[W];\n";
+  for (size_t u = 0; u < used.size() && u < static_cast<size_t>(ahead); ++u) load(u);
   for (size_t u = 0; u < used.size(); ++u) {
     const int j = used[u];
     if (u + ahead < used.size()) load(u + ahead);
@@ -459,14 +436,6 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
         s << "      " << acc << " = " << xor_chain(t) << ";\n";
         live[r][b] = true;
       }
-    s << "    }\n";
-    if (fenced) s << "    __builtin_amdgcn_sched_barrier(0);\n";
-  }
-  if (xtile) {
-    // the next tile's first inputs (the last tile re-reads its own: loads stay unconditional)
-    s << "    {\n    const unsigned tn = t + nb < nt ? t + nb : t, sn = tn / tps;\n    const long long bn = " << at("tn", "sn")
-      << ";\n";
-    for (size_t u = 0; u < first; ++u) load_at(u, "sn", "bn");
     s << "    }\n";
     if (fenced) s << "    __builtin_amdgcn_sched_barrier(0);\n";
   }

@@ -425,8 +425,8 @@ static int gf_invert(int n, int w, uint32_t *a, uint32_t *inv)
 int eco_matrix_decode(int k, int m, int w, const int *M, const int *erasures, char **ptrs, int size)
 {
     eco_init();
-    int erased[512], ids[256];
-    if (k + m > 512 || to_erased(k, m, erasures, erased)) return -1;
+    int erased[2048], ids[2048];
+    if (k + m > 2048 || to_erased(k, m, erasures, erased)) return -1;
     int n = 0;
     for (int i = 0; n < k; i++) if (!erased[i]) ids[n++] = i;
     uint32_t *a = (uint32_t *)malloc(sizeof(uint32_t) * k * k), *inv = (uint32_t *)malloc(sizeof(uint32_t) * k * k);
@@ -477,8 +477,8 @@ static int gf2_invert(int n, int *a, int *inv)
 int eco_bitmatrix_decode(int k, int m, int w, const int *B, const int *erasures, char **ptrs,
                          int size, int packet)
 {
-    int erased[512], ids[256];
-    if (k + m > 512 || to_erased(k, m, erasures, erased)) return -1;
+    int erased[2048], ids[2048];
+    if (k + m > 2048 || to_erased(k, m, erasures, erased)) return -1;
     if (packet <= 0 || size % (w * packet) != 0) return -1;
     int n = 0;
     for (int i = 0; n < k; i++) if (!erased[i]) ids[n++] = i;

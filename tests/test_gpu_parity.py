@@ -441,13 +441,48 @@ def test_gfw_network_vs_oracle(cuda, method, k, m, w, size, lost):
         assert_same(host, full)
 
 
-def test_stripe_width_limits_are_errors(cuda):
-    """k + m > 256 (LSEC_MAX_DEVS) is refused with a message, never written past a table."""
-    k, m, size = 200, 57, 4096
-    with L.Plan.new(L.REED_SOL_VAN, size, k, m, 16, 8, 8) as p:
+@pytest.mark.parametrize("w,k,m", [(8, 200, 57), (16, 1000, 25), (32, 1020, 5)])
+def test_stripe_width_limits_are_errors(cuda, w, k, m):
+    """Stripes wider than the engine takes -- k + m > 256 at w = 8 (Jerasure's own limit there,
+    reed_sol.c:247-248), > 1024 at w = 16 / 32 -- are refused with a message, never written
+    past a table."""
+    size = 64
+    with L.Plan.new(L.REED_SOL_VAN, size, k, m, w, 8, 8) as p:
         st = np.zeros((1, k + m, size), np.uint8)
         with pytest.raises(L.ErasureError, match="k\\+m"):
             p.encode_stripes(st)
+
+
+@pytest.mark.parametrize("method,k,m,w,size", [
+    (L.REED_SOL_VAN, 300, 24, 16, 4104),     # 5 input groups, 3 row launches, ragged tail
+    (L.REED_SOL_VAN, 280, 6, 32, 1024),      # k + m = 286: 5 input groups, 2 row launches
+    (L.CAUCHY_GOOD, 260, 8, 16, 2 * 16 * 8),  # bit-sliced GF(2^16), packet 8
+])
+def test_wide_word_stripes_vs_oracle(cuda, method, k, m, w, size):
+    """At w = 16 / 32 Jerasure takes k + m up to 2^w (reed_sol.c:247-248, cauchy.c:139); the engine
+    takes up to 1024 there.  Encode from host and device memory, and decodes with erasures in
+    every input group, bit-exact vs the oracle restatement."""
+    import torch
+    n = 2
+    P = 8 if method == L.CAUCHY_GOOD else 0
+    rng = np.random.default_rng(k * w + m)
+    st = np.zeros((n, k + m, size), dtype=np.uint8)
+    st[:, :k] = rng.integers(0, 256, (n, k, size), dtype=np.uint8)
+    with L.Plan.new(method, size, k, m, w, P or 8, 8) as p:
+        assert p.form_encoding_matrix() == 0 and p.form_decoding_matrix() == 0
+        p.encode_stripes(st)
+        for s in range(n):
+            assert_same(st[s, k:], O.encode(method, st[s, :k], m, P, w))
+        data = torch.from_numpy(st[:, :k].copy()).cuda()
+        par = torch.zeros((n, m, size), dtype=torch.uint8, device="cuda")
+        p.encode_dev(data, par)
+        assert np.array_equal(par.cpu().numpy(), st[:, k:])
+        full = st.copy()
+        for pat in ([0], [k - 1, k + m - 1], list(range(0, k, k // min(m, 8)))[:m], [1, 65, 129, k])[: 4]:
+            pat = sorted(set(pat))[:m]
+            st[:, pat] = 0x42
+            p.decode_stripes(st, pat)
+            assert_same(st, full)
 
 
 def test_randomized_plans_vs_oracle(cuda):
