@@ -20,6 +20,8 @@
 #include <sys/syscall.h>
 #include <unistd.h>
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -737,6 +739,30 @@ struct CopyJob {
 // NUMA node whose copy pool packs this thread's staging: set by threads that work for one
 // device (its dispatcher, the threads of a split host batch), -1 elsewhere
 thread_local int tl_copy_node = -1;
+
+// Copy with non-temporal (streaming) stores: the destination is a page-locked slot the GPU
+// reads next, or a caller buffer well outside the caches, so neither is worth the
+// read-for-ownership of ordinary stores, and the GPU's reads of the slot find no dirty CPU lines
+// to snoop.  Own-slot calls at one thread: 1 MiB Cauchy(6+3) decodes 18.6-20.6 -> 21.9-22.5 GiB/s,
+// RS(6+3) 1 MiB encodes 13.7 -> 15.5, 256 KiB 11.1 -> 12.7 (profiles/r03_v25_slot_phases_nt.txt).
+// The caller issues _mm_sfence() before anything that publishes the bytes.
+void stream_copy(char *dst, const char *src, size_t n) {
+  while (n && (reinterpret_cast<uintptr_t>(dst) & 15)) {
+    *dst++ = *src++;
+    --n;
+  }
+  for (; n >= 64; n -= 64, dst += 64, src += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 32));
+    const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst), a);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + 48), d);
+  }
+  if (n) std::memcpy(dst, src, n);
+}
 
 class CopyPool {
  public:
@@ -2892,12 +2918,17 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
     ~InFlight() { n.fetch_sub(1, std::memory_order_acq_rel); }
   } inflight(slot_calls);
   const bool pool = pool_mode >= 0 ? pool_mode == 1 : inflight.at > 2;
+  static const bool nt = [] {  // LSEC_ZC_NT=0: plain memcpy for the calling thread's copies (A/B)
+    const char *v = getenv("LSEC_ZC_NT");
+    return !v || *v != '0';
+  }();
   const auto pack = [&](std::vector<CopyJob> &js) {
     if (pool) {
       CopyPool::get().run(js, 64 << 10);
       return;
     }
-    for (const CopyJob &j : js) std::memcpy(j.dst, j.src, j.bytes);
+    for (const CopyJob &j : js) nt ? stream_copy(j.dst, j.src, j.bytes) : (void)std::memcpy(j.dst, j.src, j.bytes);
+    if (nt) _mm_sfence();  // the streamed bytes are visible before the launch (or the return) that follows
   };
   if (stats) ZcStats::get().s_alloc.fetch_add(tns(tl_zc_t0, t_last), std::memory_order_relaxed);
   const auto lap = [&](std::atomic<unsigned long long> &acc) {
