@@ -764,6 +764,20 @@ void stream_copy(char *dst, const char *src, size_t n) {
   if (n) std::memcpy(dst, src, n);
 }
 
+// LSEC_NT_COPY=0: plain memcpy instead of streaming stores for the host copies (A/B runs)
+bool nt_copies() {
+  static const bool on = [] {
+    const char *v = getenv("LSEC_NT_COPY");
+    return !v || *v != '0';
+  }();
+  return on;
+}
+
+void host_copy(char *dst, const char *src, size_t n) {
+  if (nt_copies()) stream_copy(dst, src, n);
+  else std::memcpy(dst, src, n);
+}
+
 class CopyPool {
  public:
   // one pool per NUMA node (workers pinned to the node's CPUs, ec_numa.h), plus an unpinned one
@@ -785,7 +799,8 @@ class CopyPool {
         pieces.push_back({j.dst + o, j.src + o, std::min(kPiece, j.bytes - o)});
     if (pieces.empty()) return;
     if (workers_.empty() || pieces.size() == 1) {
-      for (const CopyJob &j : pieces) std::memcpy(j.dst, j.src, j.bytes);
+      for (const CopyJob &j : pieces) host_copy(j.dst, j.src, j.bytes);
+      _mm_sfence();
       return;
     }
     Batch b;
@@ -843,7 +858,8 @@ class CopyPool {
   // copies pieces until none are left; the caller of work() must hold a `users` reference
   void work(Batch &b, bool worker) {
     size_t mine = 0;
-    for (size_t i; (i = b.next.fetch_add(1)) < b.n; ++mine) std::memcpy(b.jobs[i].dst, b.jobs[i].src, b.jobs[i].bytes);
+    for (size_t i; (i = b.next.fetch_add(1)) < b.n; ++mine) host_copy(b.jobs[i].dst, b.jobs[i].src, b.jobs[i].bytes);
+    _mm_sfence();  // this thread's streamed bytes are visible before the batch is reported done
     std::lock_guard<std::mutex> lk(mu_);
     b.finished += mine;
     if (worker) --b.users;
@@ -2918,17 +2934,13 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
     ~InFlight() { n.fetch_sub(1, std::memory_order_acq_rel); }
   } inflight(slot_calls);
   const bool pool = pool_mode >= 0 ? pool_mode == 1 : inflight.at > 2;
-  static const bool nt = [] {  // LSEC_ZC_NT=0: plain memcpy for the calling thread's copies (A/B)
-    const char *v = getenv("LSEC_ZC_NT");
-    return !v || *v != '0';
-  }();
   const auto pack = [&](std::vector<CopyJob> &js) {
     if (pool) {
       CopyPool::get().run(js, 64 << 10);
       return;
     }
-    for (const CopyJob &j : js) nt ? stream_copy(j.dst, j.src, j.bytes) : (void)std::memcpy(j.dst, j.src, j.bytes);
-    if (nt) _mm_sfence();  // the streamed bytes are visible before the launch (or the return) that follows
+    for (const CopyJob &j : js) host_copy(j.dst, j.src, j.bytes);
+    _mm_sfence();  // the streamed bytes are visible before the launch (or the return) that follows
   };
   if (stats) ZcStats::get().s_alloc.fetch_add(tns(tl_zc_t0, t_last), std::memory_order_relaxed);
   const auto lap = [&](std::atomic<unsigned long long> &acc) {
