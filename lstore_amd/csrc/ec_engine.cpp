@@ -2562,6 +2562,9 @@ class StripeServer {
         char *region = data_ + static_cast<size_t>(sl) * kSlotBytes;
         const uint64_t dregion = data_dev_ + static_cast<uint64_t>(sl) * kSlotBytes;
         for (size_t j = 0; j < nin; ++j) {
+          // plain stores: for these 4 KiB pieces streaming ones cost 15 -> 18 us p50 at one
+          // thread (the server reads them back from DRAM instead of the host's caches;
+          // profiles/r03_v27_fnptr_fair.jsonl)
           std::memcpy(region + j * n, ptrs[in_ids[j]] + c0, static_cast<size_t>(n));
           d.in[j] = dregion + j * n;
         }
