@@ -34,6 +34,7 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <random>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -4136,6 +4137,35 @@ long long lsec_test_server_hold(int hold, int timeout_ms) {
   if (timeout_ms > 0) g_srv_timeout_ms.store(timeout_ms);
   if (hold >= 0) StripeServer::restart_all();
   return static_cast<long long>(g_st_srv_timeouts.load());
+}
+
+// Self-test of the host copies (test hook, not in include/): stream_copy and the copy pool
+// over `cases` random (source offset, destination offset, length) triples, lengths 0..300 KiB,
+// against memcpy; bytes around each destination must stay untouched.  0 / -1.
+int lsec_selftest_copies(int cases, unsigned seed) {
+  if (cases < 1) return fail("lsec_selftest_copies: bad arguments");
+  std::mt19937 rng(seed);
+  const size_t cap = (300u << 10) + 256;
+  std::vector<char> src(cap + 64), dst(cap + 64), want(cap + 64);
+  for (auto &c : src) c = static_cast<char>(rng());
+  for (int i = 0; i < cases; ++i) {
+    const size_t so = rng() % 64, doff = rng() % 64;
+    size_t n = rng() % 4 == 0 ? rng() % 256 : rng() % (300u << 10);
+    for (auto &c : dst) c = static_cast<char>(0xA5);
+    want = dst;
+    std::memcpy(&want[doff], &src[so], n);
+    if (i % 2) {
+      stream_copy(&dst[doff], &src[so], n);
+      _mm_sfence();
+    } else {
+      std::vector<CopyJob> jobs{{&dst[doff], &src[so], n}};
+      CopyPool::get().run(jobs, 1 + rng() % (64u << 10));
+    }
+    if (std::memcmp(dst.data(), want.data(), dst.size()) != 0)
+      return fail("lsec_selftest_copies: case %d (src +%zu, dst +%zu, %zu B, %s) differs", i, so, doff, n,
+                  i % 2 ? "stream_copy" : "copy pool");
+  }
+  return 0;
 }
 
 int lsec_selftest_waits(int threads, int iters) {
