@@ -540,6 +540,13 @@ int decode_entry_locked(PlanExt *e, const std::vector<int> &ids, int dev, Decode
       ent.wrows.assign(wp.rows.begin(), wp.rows.end());
     } else if (kind == KBITMATRIX) {
       const lio_erasure_plan_t *p = &e->pub;
+      // The decode inverts the (k*w) x (k*w) survivor bitmatrix over GF(2) on the host, about
+      // (k*w)^3 / 64 word operations (Jerasure's jerasure_invert_bitmatrix does the same on ints,
+      // jerasure.c:1049-1093): seconds at k*w = 8192, tens of seconds at 16384, hours for the
+      // widest liberation plans.  Past 16384 the call fails instead of stalling its caller.
+      if (static_cast<long long>(k) * p->w > 16384)
+        return fail("decoding a %s plan with k*w = %d bits (a %d x %d GF(2) inversion) is beyond this engine",
+                    JE_method[p->method], k * p->w, k * p->w, k * p->w);
       std::vector<int> bm(p->encode_bitmatrix, p->encode_bitmatrix + static_cast<size_t>(k) * p->parity_strips * p->w * p->w);
       if (!lsec::gf8::make_bit_decode(k, p->parity_strips, p->w, bm, ids, ent.dp, ent.masks))
         return fail("decoding bitmatrix is singular");

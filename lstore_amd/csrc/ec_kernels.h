@@ -24,7 +24,9 @@ namespace lsec {
 constexpr int kMaxK = 64;   // input shards per launch (wider stripes: several launches, the later ones with
                             // ApplyArgs::accumulate, over images in the grouped layout below)
 constexpr int kMaxR = 16;   // output shards per launch
-constexpr int kMaxW = 256;  // bitmatrix word size w (packets per super-packet) the kernels accept
+constexpr int kMaxW = 257;  // bitmatrix word size w (packets per super-packet) the kernels accept:
+                             // every liberation-family plan with k + m <= 256 (liberation k = 252..254
+                             // gets w = 257, erasure_tools.c:756-757)
 
 // Matrix images of stripes wider than kMaxK inputs are stored in groups of kMaxK input columns:
 // group g (inputs g*kMaxK ..) holds every row's cells / masks / products for its columns, rows in

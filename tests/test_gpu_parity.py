@@ -95,6 +95,32 @@ def test_liberation_family_vs_reference(cuda, method, k, w):
             assert np.array_equal(sh, full), er
 
 
+def test_liberation_w257_encode_vs_reference(cuda):
+    """Liberation with k = 252 (k + m = 254) gets w = nearest_prime(252) = 257 from et_generate_plan
+    (erasure_tools.c:756-757): encoded on the any-w bitmatrix kernel, bit-exact vs the real
+    reference.  Its decode would invert a 64,764-bit-square GF(2) matrix on the host (the
+    reference's jerasure_invert_bitmatrix would need 16 GB of ints for it): the engine fails that
+    call with a message instead of stalling."""
+    if not O.ref_available():
+        pytest.skip("oracle/_ref not built")
+    k, m, w, P = 252, 2, 257, 8
+    g = L.Plan.generate(k * w * 4096 * 2, L.LIBERATION, k, m)
+    assert g.w == 257
+    g.close()
+    size = w * P * 2
+    data = stripe(k, size, w)
+    ref = O.RefPlan(L.LIBERATION, k, m, w, P).encode(data)
+    par = np.zeros((m, size), np.uint8)
+    with L.Plan.new(L.LIBERATION, size, k, m, w, P, 8) as p:
+        p.form_encoding_matrix()
+        p.encode_block([data[j] for j in range(k)] + [par[i] for i in range(m)])
+        assert np.array_equal(par, ref)
+        sh = np.vstack([data, par])
+        sh[0] = 0
+        assert p.decode_block([sh[i] for i in range(k + m)], [0]) == -1
+        assert "beyond this engine" in L.erasure.last_error()
+
+
 # ---------------------------------------------------------------- wide fields (w = 16 / 32)
 @pytest.mark.parametrize("method,k,m,w,size,P", [
     (L.REED_SOL_VAN, 6, 3, 16, 4104, 0),      # 4104 % 16 == 8: ragged last lane

@@ -227,11 +227,13 @@ def test_host_device_set_without_gpu(built):
 
 
 def test_unsupported_method_is_an_error_not_a_fallback(built):
-    with L.Plan.new(L.LIBERATION, 0, 6, 2, 257, 8, 8) as p:   # a prime w past the kernels' 256
+    with L.Plan.new(L.LIBERATION, 0, 6, 2, 263, 8, 8) as p:   # a prime w past the kernels' 257
         assert p.kernel == 0
-        st = np.zeros((1, 8, 257 * 8 * 4), np.uint8)
+        st = np.zeros((1, 8, 263 * 8 * 4), np.uint8)
         with pytest.raises(E.ErasureError, match="no GPU kernel"):
             p.encode_stripes(st)
+    with L.Plan.new(L.LIBERATION, 0, 6, 2, 257, 8, 8) as p:   # w = 257: liberation k = 252..254
+        assert p.kernel == 3
     for w in (37, 67):  # primes past the per-w kernels: the LDS-staged any-w bitmatrix kernel
         with L.Plan.new(L.LIBERATION, 0, 33, 2, w, 8, 8) as p:
             assert p.kernel == 3
