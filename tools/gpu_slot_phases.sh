@@ -13,4 +13,4 @@ for envs in "$@"; do
   env LSEC_STATS=1 ${envs//,/ } timeout -k 10 60 build/fnptr_bench "$chunk" "$threads" 3 "$method" "$op" >> "$out" 2>&1 \
     || { echo "failed: $envs"; tail -5 "$out"; exit 1; }
 done
-grep -E "^==|own-slot|gibps" "$out" | sed 's/"per_call_us_p99.*"gibps"/ ... "gibps"/' | cut -c1-300
+grep -E "^==|own-slot|server calls|gibps" "$out" | sed 's/"per_call_us_p99.*"gibps"/ ... "gibps"/' | cut -c1-300
