@@ -42,6 +42,9 @@ def main():
                     help="allocate, touch and free other host arrays (64 KiB-8 MiB) between calls, so "
                          "virtual ranges and physical pages are recycled")
     ap.add_argument("--seconds", type=float, default=0, help="run until this much time has passed (iters ignored)")
+    ap.add_argument("--caller-registered", action="store_true",
+                    help="the stripes in pageable memory the caller hipHostRegister's for the iteration and "
+                         "unregisters after it (registrations recycled, as an allocator that pins and unpins its arenas)")
     ap.add_argument("--pinned", action="store_true",
                     help="the stripes in caller page-locked memory: a fresh hipHostMalloc each iteration, the "
                          "previous one hipHostFree'd (page-locked virtual ranges recycled)")
@@ -116,6 +119,16 @@ def main():
                     hip.hipHostFree(ctypes.c_void_p(old.ctypes.data))
                     del old
                 buf = np.ctypeslib.as_array((ctypes.c_uint8 * nb).from_address(ptr.value)).reshape(n, k + m, C)
+            elif a.caller_registered:
+                import ctypes
+                hip = ctypes.CDLL("libamdhip64.so")
+                if buf is not None:
+                    hip.hipHostUnregister(ctypes.c_void_p(reg_base))
+                raw = np.empty(n * (k + m) * C + 8192, np.uint8)
+                at = (-raw.ctypes.data) % 4096
+                buf = raw[at:at + n * (k + m) * C].reshape(n, k + m, C)
+                reg_base = buf.ctypes.data
+                assert hip.hipHostRegister(ctypes.c_void_p(reg_base), ctypes.c_size_t(buf.nbytes), ctypes.c_uint(0)) == 0
             elif buf is None or not a.reuse:
                 if a.offset < 0:
                     buf = np.empty((n, k + m, C), np.uint8)
@@ -146,7 +159,7 @@ def main():
     if small is not None:
         small.close()
     print(json.dumps({"k": k, "m": m, "w": a.w, "chunk": C, "stripes": n, "iters": it, "reuse": a.reuse,
-                      "small_mix": a.small_mix, "churn": a.churn, "pinned": a.pinned, "bad_small": bad_small, "server": os.environ.get("LSEC_SERVER", ""),
+                      "small_mix": a.small_mix, "churn": a.churn, "pinned": a.pinned, "caller_registered": a.caller_registered, "bad_small": bad_small, "server": os.environ.get("LSEC_SERVER", ""),
                       "fresh_plan": a.fresh_plan, "dev_first": a.dev_first, "reg_zc": os.environ.get("LSEC_REG_ZC", ""),
                       "reg_flags": os.environ.get("LSEC_REG_FLAGS", ""), "offset": a.offset, "method": a.method, "bad_encode": bad_enc, "bad_decode": bad_dec,
                       "first_bad": first}), flush=True)
