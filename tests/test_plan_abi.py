@@ -244,3 +244,17 @@ def test_unsupported_method_is_an_error_not_a_fallback(built):
             assert p.kernel == 5   # bit-sliced GF(2^w)
     with L.Plan.generate(6 * 7 * 64 * 4, L.LIBERATION, 6, 2) as p:
         assert p.kernel == 3   # generic bitmatrix kernel
+
+
+@pytest.mark.parametrize("w,k,m,ok", [(8, 250, 6, True), (8, 250, 7, False), (16, 1000, 24, True), (16, 1000, 25, False),
+                                      (32, 1020, 4, True), (32, 1020, 5, False)])
+def test_generate_plan_width_limits(built, w, k, m, ok):
+    """k + m <= 256 at w = 8 (Jerasure's own limit there, reed_sol.c:247-248); <= 1024 for the
+    GF(2^16) / GF(2^32) matrix codes (LSEC_MAX_DEVS_WIDE): wider plans are refused at plan time."""
+    size = k * 4096
+    if ok:
+        with L.Plan.generate(size, L.REED_SOL_VAN, k, m, w) as p:
+            assert (p.k, p.m, p.w) == (k, m, w)
+    else:
+        with pytest.raises(E.ErasureError, match="k\\+m outside"):
+            L.Plan.generate(size, L.REED_SOL_VAN, k, m, w)
