@@ -3170,7 +3170,16 @@ int on_host_devices(int nstripes, size_t bytes, F &&fn) {
   return 0;
 }
 
+// The HIP runtime's last error is per thread and sticky until read; a public entry point drops
+// whatever the caller's own earlier HIP calls left there, so that the launches below, which
+// check hipGetLastError(), do not take a stale caller error for their own (seen once under
+// tools/reg_stress.py --caller-registered: "kernel launch failed: pointer does not correspond to
+// a registered memory region", left by the caller's hipHostUnregister; the call then took its
+// direct-copy retry).
+void drop_stale_error() { (void)hipGetLastError(); }
+
 int encode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C) {
+  drop_stale_error();
   PtrMemo memo;
   lio_erasure_plan_t *p = &e->pub;
   if (!ptrs) return fail("ptrs is NULL");
@@ -3200,6 +3209,7 @@ int encode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C) {
 }
 
 int decode_stripes_impl(PlanExt *e, char **ptrs, int nstripes, long long C, const int *erasures) {
+  drop_stale_error();
   PtrMemo memo;
   lio_erasure_plan_t *p = &e->pub;
   if (!ptrs) return fail("ptrs is NULL");
@@ -3920,6 +3930,7 @@ int et_decode_stripes(lio_erasure_plan_t *plan, char **ptrs, int nstripes, int b
 
 int lsec_encode_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int nstripes, long long block_size,
                     void *stream) {
+  drop_stale_error();
   PlanExt *e = ext_of(plan);
   if (!e) return fail("not an lstore_ec plan");
   if (!shards) return fail("shards is NULL");
@@ -3928,6 +3939,7 @@ int lsec_encode_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int ns
 
 int lsec_decode_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int nstripes, long long block_size,
                     const int *erasures, void *stream) {
+  drop_stale_error();
   PlanExt *e = ext_of(plan);
   if (!e) return fail("not an lstore_ec plan");
   if (!shards) return fail("shards is NULL");
@@ -3935,12 +3947,14 @@ int lsec_decode_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int ns
 }
 
 int et_encode_stripes_magic(lio_erasure_plan_t *plan, char **ptrs, int nstripes, int block_size, char *magic) {
+  drop_stale_error();
   PlanExt *e = ext_of(plan);
   if (!e) return fail("not an lstore_ec plan");
   return encode_stripes_magic_impl(e, ptrs, nstripes, block_size, reinterpret_cast<uint8_t *>(magic));
 }
 
 int et_stripes_magic(lio_erasure_plan_t *plan, char **ptrs, int nstripes, int block_size, char *magic) {
+  drop_stale_error();
   PlanExt *e = ext_of(plan);
   if (!e) return fail("not an lstore_ec plan");
   return stripes_magic_impl(e, ptrs, nstripes, block_size, reinterpret_cast<uint8_t *>(magic));
@@ -3948,6 +3962,7 @@ int et_stripes_magic(lio_erasure_plan_t *plan, char **ptrs, int nstripes, int bl
 
 int lsec_stripe_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int nstripes, long long block_size,
                           void *magic, void *stream) {
+  drop_stale_error();
   PlanExt *e = ext_of(plan);
   if (!e) return fail("not an lstore_ec plan");
   if (!shards || !magic) return fail("shards / magic is NULL");
@@ -3956,6 +3971,7 @@ int lsec_stripe_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, 
 
 int lsec_encode_magic_dev(lio_erasure_plan_t *plan, const lsec_shard_t *shards, int nstripes, long long block_size,
                           void *magic, void *stream) {
+  drop_stale_error();
   PlanExt *e = ext_of(plan);
   if (!e) return fail("not an lstore_ec plan");
   if (!shards || !magic) return fail("shards / magic is NULL");
