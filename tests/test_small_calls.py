@@ -194,3 +194,41 @@ def test_host_calls_under_memory_churn(cuda, args):
     assert out.returncode == 0, (out.stdout[-500:], out.stderr[-800:])
     rec = json.loads(out.stdout.strip().splitlines()[-1])
     assert rec["iters"] > 10 and rec["bad_encode"] == 0 and rec["bad_decode"] == 0 and rec["bad_small"] == 0, rec
+
+
+STALE_ERROR_SCRIPT = r"""
+import ctypes, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import lstore_amd as L
+import oracle as O
+hip = ctypes.CDLL("libamdhip64.so")
+junk = np.zeros(1 << 16, np.uint8)
+rng = np.random.default_rng(3)
+for C in (65536, 1 << 20):
+    p = L.Plan.for_chunk(L.CAUCHY_GOOD, 6, 3, C)
+    p.prepare_encode()
+    for _ in range(8):
+        d = rng.integers(0, 256, (9, C), dtype=np.uint8)
+        d[6:] = 0
+        # an unregister of memory that was never registered fails and leaves its error in this
+        # thread's HIP last-error slot, as the caller's own HIP calls can
+        assert hip.hipHostUnregister(ctypes.c_void_p(junk.ctypes.data)) != 0
+        p.encode_block([d[j] for j in range(9)])
+        assert np.array_equal(d[6:], O.encode(L.CAUCHY_GOOD, d[:6], 3, p.packet_size)), C
+print("ok")
+"""
+
+
+@pytest.mark.gpu
+def test_stale_caller_hip_error_is_not_taken_for_a_launch_failure(cuda):
+    """A HIP error the caller's own calls left pending (HIP keeps the last error per thread until
+    it is read) must not fail the engine's next launch: public entry points clear it first
+    (ec_engine.cpp drop_stale_error).  Before that, tools/reg_stress.py --caller-registered saw a
+    1 MiB call fail with the caller's hipHostUnregister error and take the direct-copy retry.
+    Served (64 KiB) and own-launch (1 MiB, 9 MiB per call) stripes, bit-exact, with no retry."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", STALE_ERROR_SCRIPT, root], capture_output=True, text=True,
+                         timeout=110)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), (out.stdout[-500:], out.stderr[-800:])
+    assert "retried with direct copies" not in out.stderr, out.stderr[-800:]
