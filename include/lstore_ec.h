@@ -149,6 +149,21 @@ int lsec_segment_write(lio_erasure_plan_t *plan, const char *data, int nstripes,
 struct iovec;
 int lsec_segment_write_iov(lio_erasure_plan_t *plan, const struct iovec *iov, int n_iov, int nstripes, int chunk,
                            int n_shift, long long first_stripe, char **dev);
+/* segjerase_write_func's own hand-off, with no data copy (segment/jerasure.c:1780-1858): for
+ * nstripes stripes of the scatter list `iov` (as lsec_segment_write_iov reads it), the parity
+ * goes to `parity` (caller memory, nstripes*m*C bytes, stripe-major: parity chunk r of stripe s
+ * at (s*m + r)*C, the reference's per-op parity buffer) and the stripe magics to `magic`
+ * (nstripes*4 bytes), both computed on the GPU; `out` receives 2*(k+m)*nstripes iovecs
+ * [4-byte magic | chunk] in logical chunk order (data 0..k-1 then parity 0..m-1 per stripe):
+ * the tbuf the reference hands its LUN child (:1852-1853).  Data iovecs point into the caller's
+ * pages; a stripe straddling scatter pieces is gathered into `straddle` (k*C bytes per such
+ * stripe, lsec_segment_straddle_bytes tells how many bytes); a stripe starting in an error page
+ * points at an engine-owned zero chunk.  Returns the number of iovecs, or -1. */
+int lsec_segment_encode_iov(lio_erasure_plan_t *plan, const struct iovec *iov, int n_iov, int nstripes, int chunk,
+                            char *parity, char *magic, char *straddle, long long straddle_bytes, struct iovec *out,
+                            int out_cap);
+long long lsec_segment_straddle_bytes(lio_erasure_plan_t *plan, const struct iovec *iov, int n_iov, int nstripes,
+                                      int chunk);
 
 /* Flags of the read / inspect entry points */
 #define LSEC_READ_PARANOID 1   /* verify every stripe, not only those with bad chunks */

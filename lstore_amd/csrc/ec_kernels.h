@@ -19,7 +19,26 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <tuple>
+#include <utility>
+
 namespace lsec {
+
+// Launches kernel k and returns the launch's own status (hipLaunchKernel's return value).  The
+// engine never reads the runtime's per-thread last error to learn about its launches: that error
+// is sticky until read, so a read would both take a caller's pending error for the engine's and
+// clear it from under the caller.
+template <typename T, size_t... I>
+hipError_t launch_packed(const void *k, dim3 grid, dim3 block, hipStream_t st, T &args, std::index_sequence<I...>) {
+  void *ptrs[] = {static_cast<void *>(&std::get<I>(args))..., nullptr};
+  return hipLaunchKernel(k, grid, block, ptrs, 0, st);
+}
+template <typename... KArgs, typename... Args>
+hipError_t launch_kernel(void (*k)(KArgs...), dim3 grid, dim3 block, hipStream_t st, const Args &...args) {
+  static_assert(sizeof...(KArgs) == sizeof...(Args), "argument count");
+  std::tuple<std::decay_t<KArgs>...> t(static_cast<std::decay_t<KArgs>>(args)...);
+  return launch_packed(reinterpret_cast<const void *>(k), grid, block, st, t, std::index_sequence_for<KArgs...>{});
+}
 
 constexpr int kMaxK = 64;   // input shards per launch (wider stripes: several launches, the later ones with
                             // ApplyArgs::accumulate, over images in the grouped layout below)

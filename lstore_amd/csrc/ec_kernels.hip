@@ -343,15 +343,13 @@ __global__ __launch_bounds__(64) void k_signal(unsigned *counter, unsigned *flag
 
 hipError_t launch_signal(unsigned *counter, unsigned *flag, unsigned value, hipStream_t st) {
   if (!counter || !flag) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_signal, dim3(kSignalBlocks), dim3(64), 0, st, counter, flag, value);
-  return hipGetLastError();
+  return launch_kernel(&k_signal, dim3(kSignalBlocks), dim3(64), st, counter, flag, value);
 }
 
 hipError_t launch_copy_pieces(const CopyPiece *list, int n, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   // the grid does not matter from 64 to 4096 blocks (profiles/r01_v28_kcopy_grid.txt)
-  hipLaunchKernelGGL(k_copy_pieces, dim3(std::min(n, kCopyGrid)), dim3(kBlock), 0, st, list, n);
-  return hipGetLastError();
+  return launch_kernel(&k_copy_pieces, dim3(std::min(n, kCopyGrid)), dim3(kBlock), st, list, n);
 }
 
 hipError_t launch_hbm_copy(void *dst, const void *src, uint64_t bytes, hipStream_t st) {
@@ -360,9 +358,8 @@ hipError_t launch_hbm_copy(void *dst, const void *src, uint64_t bytes, hipStream
   const uint64_t n16 = bytes / 16, ntiles = (n16 + kBlock * 2 - 1) / (kBlock * 2);
   if (ntiles == 0) return hipSuccess;
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_hbm_copy, dim3(default_grid(ntiles)), dim3(kBlock), 0, st, reinterpret_cast<uint64_t>(dst),
+  return launch_kernel(&k_hbm_copy, dim3(default_grid(ntiles)), dim3(kBlock), st, reinterpret_cast<uint64_t>(dst),
                      reinterpret_cast<uint64_t>(src), n16);
-  return hipGetLastError();
 }
 
 hipError_t launch_hbm_mix(const ApplyArgs &a, hipStream_t st) {
@@ -371,14 +368,12 @@ hipError_t launch_hbm_mix(const ApplyArgs &a, hipStream_t st) {
   const uint64_t tile = kBlock * 16 * 2;
   const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_hbm_mix, dim3(default_grid(ntiles)), dim3(kBlock), 0, st, a);
-  return hipGetLastError();
+  return launch_kernel(&k_hbm_mix, dim3(default_grid(ntiles)), dim3(kBlock), st, a);
 }
 
 hipError_t launch_gather(const GatherPiece *list, int n, char *dst, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_gather, dim3(n), dim3(kBlock), 0, st, list, dst);
-  return hipGetLastError();
+  return launch_kernel(&k_gather, dim3(n), dim3(kBlock), st, list, dst);
 }
 
 hipError_t launch_chunk_diff(const DiffArgs &a, hipStream_t st) {
@@ -387,8 +382,7 @@ hipError_t launch_chunk_diff(const DiffArgs &a, hipStream_t st) {
   const uint64_t tile = kBlock * 16 * 2;
   const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_chunk_diff, dim3(default_grid(ntiles)), dim3(kBlock), 0, st, a);
-  return hipGetLastError();
+  return launch_kernel(&k_chunk_diff, dim3(default_grid(ntiles)), dim3(kBlock), st, a);
 }
 
 hipError_t launch_stripe_magic(const MagicArgs &a, hipStream_t st) {
@@ -397,16 +391,14 @@ hipError_t launch_stripe_magic(const MagicArgs &a, hipStream_t st) {
   const uint64_t tile = kBlock * 16 * 2;
   const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31) || a.size == 0) return a.size == 0 ? hipSuccess : hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_stripe_magic, dim3(default_grid(ntiles)), dim3(kBlock), 0, st, a);
-  return hipGetLastError();
+  return launch_kernel(&k_stripe_magic, dim3(default_grid(ntiles)), dim3(kBlock), st, a);
 }
 
 hipError_t launch_magic_finalize(const unsigned long long *acc, int nstripes, int64_t total_len, uint8_t *magic,
                                  hipStream_t st) {
   if (nstripes <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_magic_finalize, dim3((nstripes + 255) / 256), dim3(256), 0, st, acc, nstripes,
+  return launch_kernel(&k_magic_finalize, dim3((nstripes + 255) / 256), dim3(256), st, acc, nstripes,
                      static_cast<uint64_t>(total_len), magic);
-  return hipGetLastError();
 }
 
 }  // namespace lsec

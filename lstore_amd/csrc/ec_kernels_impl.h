@@ -980,12 +980,11 @@ template <int R, int IT, bool BF, int VW>
 hipError_t bytewise_k(const ApplyArgs &a, hipStream_t st, int grid) {
   switch (a.K) {
 #define LSEC_BW_K(KK) \
-  case KK: hipLaunchKernelGGL((k_gf8_bytewise<R, KK, IT, BF, VW>), dim3(grid), dim3(kBlock), 0, st, a); break;
+  case KK: return launch_kernel(&k_gf8_bytewise<R, KK, IT, BF, VW>, dim3(grid), dim3(kBlock), st, a);
     LSEC_BW_K(4) LSEC_BW_K(6) LSEC_BW_K(8) LSEC_BW_K(10) LSEC_BW_K(12) LSEC_BW_K(16) LSEC_BW_K(20)
 #undef LSEC_BW_K
-    default: hipLaunchKernelGGL((k_gf8_bytewise<R, 0, IT, BF, VW>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    default: return launch_kernel(&k_gf8_bytewise<R, 0, IT, BF, VW>, dim3(grid), dim3(kBlock), st, a);
   }
-  return hipGetLastError();
 }
 
 // Bytewise launch shapes (tile per lane):  code -> (IT, VW, coefficient path)
@@ -1000,8 +999,7 @@ inline int bw_shape_vw(int shape) { return shape <= 1 ? 4 : 2; }
 template <int R>
 hipError_t dispatch_bytewise(const ApplyArgs &a, hipStream_t st, int grid, int shape) {
   if (a.accumulate) {  // a later input group of a wide stripe: generic K, 16 B per lane (shape 1)
-    hipLaunchKernelGGL((k_gf8_bytewise<R, 0, 1, true, 4, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
-    return hipGetLastError();
+    return launch_kernel(&k_gf8_bytewise<R, 0, 1, true, 4, false, true>, dim3(grid), dim3(kBlock), st, a);
   }
   switch (shape) {
     case 1: return bytewise_k<R, 1, true, 4>(a, st, grid);
@@ -1018,50 +1016,44 @@ template <int R>
 hipError_t dispatch_bytewise_magic(const ApplyArgs &a, hipStream_t st, int grid) {
   switch (a.K) {
 #define LSEC_BWM_K(KK, IT) \
-  case KK: hipLaunchKernelGGL((k_gf8_bytewise<R, KK, IT, true, 4, true>), dim3(grid), dim3(kBlock), 0, st, a); break;
+  case KK: return launch_kernel(&k_gf8_bytewise<R, KK, IT, true, 4, true>, dim3(grid), dim3(kBlock), st, a);
     LSEC_BWM_K(4, 2) LSEC_BWM_K(6, 2) LSEC_BWM_K(8, 2) LSEC_BWM_K(10, 2) LSEC_BWM_K(12, 2) LSEC_BWM_K(16, 1) LSEC_BWM_K(20, 1)
 #undef LSEC_BWM_K
     default:
-      if (a.K >= 16) hipLaunchKernelGGL((k_gf8_bytewise<R, 0, 1, true, 4, true>), dim3(grid), dim3(kBlock), 0, st, a);
-      else hipLaunchKernelGGL((k_gf8_bytewise<R, 0, 2, true, 4, true>), dim3(grid), dim3(kBlock), 0, st, a);
+      if (a.K >= 16) return launch_kernel(&k_gf8_bytewise<R, 0, 1, true, 4, true>, dim3(grid), dim3(kBlock), st, a);
+      else return launch_kernel(&k_gf8_bytewise<R, 0, 2, true, 4, true>, dim3(grid), dim3(kBlock), st, a);
       break;
   }
-  return hipGetLastError();
 }
 
 template <int R>
 hipError_t dispatch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid, int dw) {
   if (a.magic_acc) {  // encode + stripe magic, one lane dword wide
-    hipLaunchKernelGGL((k_gf8_bitsliced<R, 0, 1, true>), dim3(grid), dim3(kBlock), 0, st, a);
-    return hipGetLastError();
+    return launch_kernel(&k_gf8_bitsliced<R, 0, 1, true>, dim3(grid), dim3(kBlock), st, a);
   }
   if (a.accumulate) {  // a later input group of a wide stripe, one lane dword wide
-    hipLaunchKernelGGL((k_gf8_bitsliced<R, 0, 1, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
-    return hipGetLastError();
+    return launch_kernel(&k_gf8_bitsliced<R, 0, 1, false, true>, dim3(grid), dim3(kBlock), st, a);
   }
   switch (dw) {
-    case 4: hipLaunchKernelGGL((k_gf8_bitsliced<R, 0, 4>), dim3(grid), dim3(kBlock), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((k_gf8_bitsliced<R, 0, 2>), dim3(grid), dim3(kBlock), 0, st, a); break;
-    default: hipLaunchKernelGGL((k_gf8_bitsliced<R, 0, 1>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    case 4: return launch_kernel(&k_gf8_bitsliced<R, 0, 4>, dim3(grid), dim3(kBlock), st, a);
+    case 2: return launch_kernel(&k_gf8_bitsliced<R, 0, 2>, dim3(grid), dim3(kBlock), st, a);
+    default: return launch_kernel(&k_gf8_bitsliced<R, 0, 1>, dim3(grid), dim3(kBlock), st, a);
   }
-  return hipGetLastError();
 }
 
 template <int R>
 hipError_t dispatch_bitmatrix(const ApplyArgs &a, hipStream_t st, int grid) {
   if constexpr (R <= 2) {
     if (a.accumulate) {  // wide stripes (k > 64) only occur at w > 64: the any-w kernel
-      hipLaunchKernelGGL((k_bitmatrix_any<R>), dim3(grid), dim3(kBlock), 0, st, a);
-      return hipGetLastError();
+      return launch_kernel(&k_bitmatrix_any<R>, dim3(grid), dim3(kBlock), st, a);
     }
     switch (a.w) {
 #define LSEC_BM_W(WW) \
-  case WW: hipLaunchKernelGGL((k_bitmatrix<R, WW>), dim3(grid), dim3(kBlock), 0, st, a); break;
+  case WW: return launch_kernel(&k_bitmatrix<R, WW>, dim3(grid), dim3(kBlock), st, a);
       LSEC_BITMATRIX_W(LSEC_BM_W)
 #undef LSEC_BM_W
-      default: hipLaunchKernelGGL((k_bitmatrix_any<R>), dim3(grid), dim3(kBlock), 0, st, a); break;
+      default: return launch_kernel(&k_bitmatrix_any<R>, dim3(grid), dim3(kBlock), st, a);
     }
-    return hipGetLastError();
   } else {
     return hipErrorInvalidValue;
   }
@@ -1070,44 +1062,41 @@ hipError_t dispatch_bitmatrix(const ApplyArgs &a, hipStream_t st, int grid) {
 template <int R>
 hipError_t dispatch_wordwise(const ApplyArgs &a, hipStream_t st, int grid) {
   switch (a.w * 2 + (a.accumulate ? 1 : 0)) {
-    case 32: hipLaunchKernelGGL((k_gfw_wordwise<R, 16>), dim3(grid), dim3(kBlock), 0, st, a); break;
-    case 33: hipLaunchKernelGGL((k_gfw_wordwise<R, 16, true>), dim3(grid), dim3(kBlock), 0, st, a); break;
-    case 64: hipLaunchKernelGGL((k_gfw_wordwise<R, 32>), dim3(grid), dim3(kBlock), 0, st, a); break;
-    case 65: hipLaunchKernelGGL((k_gfw_wordwise<R, 32, true>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    case 32: return launch_kernel(&k_gfw_wordwise<R, 16>, dim3(grid), dim3(kBlock), st, a);
+    case 33: return launch_kernel(&k_gfw_wordwise<R, 16, true>, dim3(grid), dim3(kBlock), st, a);
+    case 64: return launch_kernel(&k_gfw_wordwise<R, 32>, dim3(grid), dim3(kBlock), st, a);
+    case 65: return launch_kernel(&k_gfw_wordwise<R, 32, true>, dim3(grid), dim3(kBlock), st, a);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 // at most 8 rows per launch at w = 16, 4 at w = 32 (acc[R][W] lives in VGPRs)
 template <int R>
 hipError_t dispatch_gfw_transposed(const ApplyArgs &a, hipStream_t st, int grid) {
   if (a.w == 16) {
-    if (a.accumulate) hipLaunchKernelGGL((k_gfw_transposed<R, 16, true>), dim3(grid), dim3(kBlock), 0, st, a);
-    else hipLaunchKernelGGL((k_gfw_transposed<R, 16>), dim3(grid), dim3(kBlock), 0, st, a);
+    if (a.accumulate) return launch_kernel(&k_gfw_transposed<R, 16, true>, dim3(grid), dim3(kBlock), st, a);
+    else return launch_kernel(&k_gfw_transposed<R, 16>, dim3(grid), dim3(kBlock), st, a);
   } else if constexpr (R <= 4) {
     if (a.w != 32) return hipErrorInvalidValue;
-    if (a.accumulate) hipLaunchKernelGGL((k_gfw_transposed<R, 32, true>), dim3(grid), dim3(kBlock), 0, st, a);
-    else hipLaunchKernelGGL((k_gfw_transposed<R, 32>), dim3(grid), dim3(kBlock), 0, st, a);
+    if (a.accumulate) return launch_kernel(&k_gfw_transposed<R, 32, true>, dim3(grid), dim3(kBlock), st, a);
+    else return launch_kernel(&k_gfw_transposed<R, 32>, dim3(grid), dim3(kBlock), st, a);
   } else {
     return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 template <int R>
 hipError_t dispatch_gfw_bitsliced(const ApplyArgs &a, hipStream_t st, int grid) {
   if (a.w == 16) {
-    if (a.accumulate) hipLaunchKernelGGL((k_gfw_bitsliced<R, 16, true>), dim3(grid), dim3(kBlock), 0, st, a);
-    else hipLaunchKernelGGL((k_gfw_bitsliced<R, 16>), dim3(grid), dim3(kBlock), 0, st, a);
+    if (a.accumulate) return launch_kernel(&k_gfw_bitsliced<R, 16, true>, dim3(grid), dim3(kBlock), st, a);
+    else return launch_kernel(&k_gfw_bitsliced<R, 16>, dim3(grid), dim3(kBlock), st, a);
   } else if constexpr (R <= 4) {
     if (a.w != 32) return hipErrorInvalidValue;
-    if (a.accumulate) hipLaunchKernelGGL((k_gfw_bitsliced<R, 32, true>), dim3(grid), dim3(kBlock), 0, st, a);
-    else hipLaunchKernelGGL((k_gfw_bitsliced<R, 32>), dim3(grid), dim3(kBlock), 0, st, a);
+    if (a.accumulate) return launch_kernel(&k_gfw_bitsliced<R, 32, true>, dim3(grid), dim3(kBlock), st, a);
+    else return launch_kernel(&k_gfw_bitsliced<R, 32>, dim3(grid), dim3(kBlock), st, a);
   } else {
     return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 #define LSEC_DECLARE_R(RR)                                                                         \

@@ -15,6 +15,7 @@ namespace lsec {
 constexpr int kSrvWG = LSEC_SRV_WG;  // server workgroups (one per CU they land on)
 constexpr int kSrvSlotsPerWG = 31;  // post words 0-30 (two 64-byte lines); word 31 is the stop word
 constexpr int kSrvSlots = kSrvWG * kSrvSlotsPerWG;
+constexpr size_t kSrvSlotBytes = 96u << 10;  // chunk bytes of one slot (a part's inputs + outputs)
 constexpr int kSrvMaxK = 32;        // inputs of one request the server takes
 constexpr int kSrvMaxR = 8;         // outputs of one request the server takes
 constexpr uint32_t kSrvBytewise = 1, kSrvBitsliced = 2;

@@ -176,6 +176,11 @@ __global__ __launch_bounds__(kBlock) void k_stripe_server(SrvArgs a) {
       const uint32_t val = __shfl(v, first < 0 ? 0 : first);
       if (lane == 0) {
         int q = stop != 0;
+        // The stop word is final: from the poll that sees it, nothing more is picked, so the
+        // launch leaves after at most the part each workgroup is serving now, however busy the
+        // posting threads keep the slots.  What is still posted waits for the next launch, which
+        // reloads served[] from done[] (the host cancels the stopping call's own parts).
+        if (q) first = -1;
         if (first >= 0 && voted) {
           // work again: take back the idle vote before serving -- unless the count is complete.
           // Retirement is a one-way latch: once every workgroup has voted, a workgroup that has
@@ -263,8 +268,7 @@ __global__ __launch_bounds__(kBlock) void k_stripe_server(SrvArgs a) {
 
 hipError_t launch_stripe_server(const SrvArgs &a, hipStream_t st) {
   if (!a.shared || !a.votes) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_stripe_server, dim3(kSrvWG), dim3(kBlock), 0, st, a);
-  return hipGetLastError();
+  return launch_kernel(&k_stripe_server, dim3(kSrvWG), dim3(kBlock), st, a);
 }
 
 }  // namespace lsec

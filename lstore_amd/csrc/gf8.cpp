@@ -289,8 +289,136 @@ bool make_decode(int k, int m, const Mat &coding, const std::vector<int> &erased
   return true;
 }
 
+namespace {
+
+using BitRow = std::vector<uint64_t>;
+
+bool bit_at(const BitRow &r, int c) { return (r[c / 64] >> (c % 64)) & 1; }
+void set_bit(BitRow &r, int c) { r[c / 64] |= 1ull << (c % 64); }
+void xor_into(BitRow &dst, const BitRow &src) {
+  for (size_t x = 0; x < dst.size(); ++x) dst[x] ^= src[x];
+}
+
+// survivors / erased as make_decode (first k surviving ids, jerasure.c:100-128)
+bool pick_survivors(int k, int m, const std::vector<int> &erased_ids, DecodePlan &dp) {
+  std::vector<char> lost(k + m, 0);
+  for (int e : erased_ids) {
+    if (e < 0 || e >= k + m) return false;
+    lost[e] = 1;
+  }
+  dp.erased.clear();
+  dp.survivors.clear();
+  for (int i = 0; i < k + m; ++i) {
+    if (lost[i]) dp.erased.push_back(i);
+    else if (static_cast<int>(dp.survivors.size()) < k) dp.survivors.push_back(i);
+  }
+  return static_cast<int>(dp.survivors.size()) == k;
+}
+
+// rows[(r*w + l)] over survivor bit columns -> the kernels' mask layout
+void rows_to_masks(int k, int w, const std::vector<BitRow> &rows, std::vector<uint32_t> &masks) {
+  const int nw = (w + 31) / 32;  // mask words per (bit-row, input), as lsec::mask_words
+  const int n = k * w;
+  masks.assign(rows.size() * k * nw, 0u);
+  for (size_t rl = 0; rl < rows.size(); ++rl)
+    for (int c = 0; c < n; ++c)
+      if (bit_at(rows[rl], c)) masks[(rl * k + c / w) * nw + (c % w) / 32] |= 1u << (c % w % 32);
+}
+
+}  // namespace
+
+// Solves only for the lost data bits.  With d data strips lost, the survivors are the k - d
+// surviving data strips plus d coding strips (pick_survivors), so the unknowns are the d*w lost
+// data bits and the equations the d*w bit-rows of those coding strips:
+//   B_L . data_L = coding_P + B_D . data_D        (GF(2): minus is plus)
+// A = B_L is (d*w) x (d*w); data_L = A^-1 . (coding_P + B_D . data_D), written over survivor bit
+// columns.  A lost coding strip is re-encoded from data expressed the same way.  This is the
+// decoding matrix jerasure_generate_decoding_schedule builds (jerasure.c:823-951) without its
+// (k*w) x (k*w) inversion: O((d*w)^3 + (d*w)^2 * k*w / 64) word operations instead of
+// O((k*w)^3 / 64), so liberation plans up to k = 254, w = 257 decode in well under a second.
+// Decoded bytes are unique (the codes are MDS), so the rows equal make_bit_decode_dense's.
 bool make_bit_decode(int k, int m, int w, const std::vector<int> &bm, const std::vector<int> &erased_ids,
                      DecodePlan &dp, std::vector<uint32_t> &masks) {
+  if (!pick_survivors(k, m, erased_ids, dp)) return false;
+  const int n = k * w;
+  const int words = (n + 63) / 64;
+  std::vector<int> pos(k + m, -1);  // survivor index of a device id
+  for (int j = 0; j < k; ++j) pos[dp.survivors[j]] = j;
+  std::vector<int> lost_data, used_coding;
+  for (int id : dp.erased)
+    if (id < k) lost_data.push_back(id);
+  for (int id : dp.survivors)
+    if (id >= k) used_coding.push_back(id);
+  const int d = static_cast<int>(lost_data.size());
+  if (static_cast<int>(used_coding.size()) != d) return false;
+  const auto brow = [&](int id, int l) { return &bm[static_cast<size_t>((id - k) * w + l) * n]; };
+  // known part of a coding bit-row over survivor columns: the row's surviving-data bits
+  const auto data_part = [&](int id, int l, BitRow &row) {
+    const int *src = brow(id, l);
+    for (int j = 0; j < k; ++j) {
+      if (pos[j] < 0) continue;
+      for (int x = 0; x < w; ++x)
+        if (src[j * w + x]) set_bit(row, pos[j] * w + x);
+    }
+  };
+  std::vector<BitRow> lost_rows(static_cast<size_t>(d) * w, BitRow(words, 0));  // lost data bit (u, x)
+  if (d > 0) {
+    const int dw = d * w, aw = (dw + 63) / 64;
+    std::vector<BitRow> a(dw, BitRow(aw, 0)), ainv(dw, BitRow(aw, 0));
+    std::vector<BitRow> rhs(dw, BitRow(words, 0));  // coding_P + B_D . data_D over survivor columns
+    for (int t = 0; t < d; ++t)
+      for (int l = 0; l < w; ++l) {
+        const int row = t * w + l;
+        const int *src = brow(used_coding[t], l);
+        for (int u = 0; u < d; ++u)
+          for (int x = 0; x < w; ++x)
+            if (src[lost_data[u] * w + x]) set_bit(a[row], u * w + x);
+        set_bit(rhs[row], pos[used_coding[t]] * w + l);
+        data_part(used_coding[t], l, rhs[row]);
+      }
+    for (int i = 0; i < dw; ++i) set_bit(ainv[i], i);
+    for (int c = 0; c < dw; ++c) {  // Gauss-Jordan over GF(2)
+      int p = c;
+      while (p < dw && !bit_at(a[p], c)) ++p;
+      if (p == dw) return false;
+      std::swap(a[p], a[c]);
+      std::swap(ainv[p], ainv[c]);
+      for (int r = 0; r < dw; ++r)
+        if (r != c && bit_at(a[r], c)) {
+          xor_into(a[r], a[c]);
+          xor_into(ainv[r], ainv[c]);
+        }
+    }
+    for (int r = 0; r < dw; ++r)
+      for (int c = 0; c < dw; ++c)
+        if (bit_at(ainv[r], c)) xor_into(lost_rows[r], rhs[c]);
+  }
+  std::vector<int> lost_index(k, -1);
+  for (int u = 0; u < d; ++u) lost_index[lost_data[u]] = u;
+  std::vector<BitRow> out;
+  out.reserve(dp.erased.size() * w);
+  for (int id : dp.erased)
+    for (int l = 0; l < w; ++l) {
+      if (id < k) {
+        out.push_back(lost_rows[static_cast<size_t>(lost_index[id]) * w + l]);
+        continue;
+      }
+      BitRow row(words, 0);
+      data_part(id, l, row);
+      const int *src = brow(id, l);
+      for (int u = 0; u < d; ++u)
+        for (int x = 0; x < w; ++x)
+          if (src[lost_data[u] * w + x]) xor_into(row, lost_rows[static_cast<size_t>(u) * w + x]);
+      out.push_back(std::move(row));
+    }
+  rows_to_masks(k, w, out, masks);
+  return true;
+}
+
+// The whole (k*w) x (k*w) survivor bitmatrix inverted, as jerasure_invert_bitmatrix does
+// (jerasure.c:1049-1104).  Test comparator of make_bit_decode (lsec_selftest_bit_decode).
+bool make_bit_decode_dense(int k, int m, int w, const std::vector<int> &bm, const std::vector<int> &erased_ids,
+                           DecodePlan &dp, std::vector<uint32_t> &masks) {
   std::vector<char> lost(k + m, 0);
   for (int e : erased_ids) {
     if (e < 0 || e >= k + m) return false;

@@ -76,7 +76,8 @@ class ShardRef(C.Structure):
 EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan", "et_destroy_plan",
            "et_encode", "et_decode", "et_encode_stripes", "et_decode_stripes", "lsec_encode_dev",
            "lsec_decode_dev", "et_encode_stripes_magic", "et_stripes_magic", "lsec_encode_magic_dev",
-           "lsec_stripe_magic_dev", "lsec_segment_write", "lsec_segment_write_iov", "lsec_segment_read", "lsec_segment_inspect",
+           "lsec_stripe_magic_dev", "lsec_segment_write", "lsec_segment_write_iov", "lsec_segment_encode_iov",
+           "lsec_segment_straddle_bytes", "lsec_segment_read", "lsec_segment_inspect",
            "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count", "lsec_last_error", "lsec_plan_kernel",
            "lsec_set_kernel_variant", "lsec_set_host_devices", "lsec_hbm_copy_dev", "lsec_hbm_mix_dev", "lsec_prepare_encode", "lsec_plan_jit", "lsec_device_numa")
 
@@ -140,6 +141,10 @@ def lib():
     L.lsec_stripe_magic_dev.argtypes = [P, C.POINTER(ShardRef), C.c_int, C.c_longlong, C.c_void_p, C.c_void_p]
     L.lsec_segment_write.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_void_p]
     L.lsec_segment_write_iov.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_void_p]
+    L.lsec_segment_encode_iov.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_longlong, C.c_void_p, C.c_int]
+    L.lsec_segment_straddle_bytes.restype = C.c_longlong
+    L.lsec_segment_straddle_bytes.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int]
     L.lsec_segment_read.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_int, C.c_void_p,
                                     C.c_void_p]
     L.lsec_segment_inspect.argtypes = [P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -349,12 +354,15 @@ class Plan:
                                            _stream_handle(stream)), "lsec_stripe_magic_dev")
 
     # -- segment adapter (segjerase_write_func + LUN placement)
-    def segment_write(self, data: np.ndarray, n_shift: int = 1, first_stripe: int = 0) -> np.ndarray:
-        """data uint8 [N, k, C] -> device images uint8 [k+m, N*(C+4)] (lsec_segment_write)."""
+    def segment_write(self, data: np.ndarray, n_shift: int = 1, first_stripe: int = 0,
+                      out: "np.ndarray | None" = None) -> np.ndarray:
+        """data uint8 [N, k, C] -> device images uint8 [k+m, N*(C+4)] (lsec_segment_write), written
+        into `out` when given (the depots' buffers, reused across calls)."""
         n_str, k, size = data.shape
         n = self.k + self.m
         data = np.ascontiguousarray(data)
-        dev = np.zeros((n, n_str * (size + 4)), dtype=np.uint8)
+        dev = out if out is not None else np.zeros((n, n_str * (size + 4)), dtype=np.uint8)
+        assert dev.shape == (n, n_str * (size + 4)) and dev.dtype == np.uint8 and dev.flags.c_contiguous
         ptrs = self._ptr_array([dev[i].ctypes.data for i in range(n)])
         _check(lib().lsec_segment_write(self._p, data.ctypes.data, n_str, size, n_shift, first_stripe, ptrs),
                "lsec_segment_write")
@@ -379,6 +387,43 @@ class Plan:
         _check(lib().lsec_segment_write_iov(self._p, iov, len(pieces), nstripes, chunk, n_shift, first_stripe, ptrs),
                "lsec_segment_write_iov")
         return dev
+
+    @staticmethod
+    def _iov_array(pieces):
+        iov = (IoVec * max(1, len(pieces)))()
+        keep = []
+        for i, pc in enumerate(pieces):
+            if isinstance(pc, (int, np.integer)):
+                iov[i].iov_base, iov[i].iov_len = None, int(pc)
+            else:
+                pc = np.ascontiguousarray(pc, dtype=np.uint8)
+                keep.append(pc)
+                iov[i].iov_base, iov[i].iov_len = pc.ctypes.data, pc.nbytes
+        return iov, keep
+
+    def segment_encode_iov(self, pieces, nstripes: int, chunk: int, parity: "np.ndarray | None" = None,
+                           magic: "np.ndarray | None" = None):
+        """segjerase_write_func's hand-off with no data copy (lsec_segment_encode_iov): pieces as for
+        segment_write_iov.  Returns (iovs, parity uint8 [N, m, C], magic uint8 [N, 4], keep): iovs
+        is a uint64 [2(k+m)N, 2] view of the iovecs [magic | chunk] in logical order (rows of address,
+        length); `keep` holds what they point into (the pieces' arrays, the straddle buffer) and
+        the iovec array itself."""
+        n = self.k + self.m
+        iov, keep = self._iov_array(pieces)
+        par = parity if parity is not None else np.empty((nstripes, self.m, chunk), np.uint8)
+        mag = magic if magic is not None else np.empty((nstripes, 4), np.uint8)
+        assert par.nbytes >= nstripes * self.m * chunk and mag.nbytes >= nstripes * 4
+        sb = lib().lsec_segment_straddle_bytes(self._p, iov, len(pieces), nstripes, chunk)
+        if sb < 0:
+            raise ErasureError(f"lsec_segment_straddle_bytes failed: {last_error()}")
+        straddle = np.empty(max(1, sb), np.uint8)
+        out = (IoVec * max(1, 2 * n * nstripes))()
+        got = lib().lsec_segment_encode_iov(self._p, iov, len(pieces), nstripes, chunk, par.ctypes.data, mag.ctypes.data,
+                                            straddle.ctypes.data, sb, out, 2 * n * nstripes)
+        if got != 2 * n * nstripes:
+            raise ErasureError(f"lsec_segment_encode_iov failed (rc={got}): {last_error()}")
+        iovs = np.frombuffer(out, dtype=np.uint64).reshape(-1, 2)[:got]  # rows (address, length), no copy
+        return iovs, par, mag, keep + [straddle, out]
 
     def segment_read(self, dev: np.ndarray, nstripes: int, chunk: int, n_shift: int = 1, first_stripe: int = 0,
                      paranoid: bool = False, missing=(), legacy_magic: bool = False):

@@ -220,11 +220,12 @@ class RefPlan:
         return self.lib.ref_plan_decode(self.h, _ptrs([shards[i] for i in range(km)]), size,
                                         _iarr(list(erasures) + [-1]))
 
-    def segment_write(self, data, nstripes, chunk, n_shift=1, first_stripe=0):
+    def segment_write(self, data, nstripes, chunk, n_shift=1, first_stripe=0, out=None):
         """segjerase_write_func + LUN placement restated over the real jerasure (config c1).
-        data: uint8 [nstripes, k, C]; returns uint8 [k+m, nstripes*(C+4)] device images."""
+        data: uint8 [nstripes, k, C]; returns uint8 [k+m, nstripes*(C+4)] device images (into
+        `out` when given)."""
         n = self.k + self.m
-        dev = np.zeros((n, nstripes * (chunk + 4)), dtype=np.uint8)
+        dev = out if out is not None else np.zeros((n, nstripes * (chunk + 4)), dtype=np.uint8)
         ptrs = _ptrs([dev[i] for i in range(n)])
         data = np.ascontiguousarray(data)
         self.lib.ref_segment_write(self.h, data.ctypes.data, nstripes, chunk, n_shift, first_stripe, ptrs)

@@ -95,17 +95,21 @@ def test_liberation_family_vs_reference(cuda, method, k, w):
             assert np.array_equal(sh, full), er
 
 
-def test_liberation_w257_encode_vs_reference(cuda):
-    """Liberation with k = 252 (k + m = 254) gets w = nearest_prime(252) = 257 from et_generate_plan
-    (erasure_tools.c:756-757): encoded on the any-w bitmatrix kernel, bit-exact vs the real
-    reference.  Its decode would invert a 64,764-bit-square GF(2) matrix on the host (the
-    reference's jerasure_invert_bitmatrix would need 16 GB of ints for it): the engine fails that
-    call with a message instead of stalling."""
+@pytest.mark.parametrize("k", [128, 252])
+def test_wide_liberation_decodes_round_trip(cuda, k):
+    """Liberation with k = 128 (w = 131) and k = 252 (k + m = 254, w = nearest_prime(252) = 257
+    from et_generate_plan, erasure_tools.c:756-757): encoded on the any-w bitmatrix kernel,
+    bit-exact vs the real reference; then every kind of loss decodes back to the encoded bytes.
+    The reference would decode lost data by inverting the whole (k*w)-square survivor bitmatrix
+    (jerasure_invert_bitmatrix, jerasure.c:1049; 16 GB of ints at k = 252), which cannot finish
+    here, so decode parity rests on the round trip (the MDS code's recovered bytes are unique)
+    plus tests/test_bit_decode.py's rows-equal-the-dense-inversion check at small k."""
     if not O.ref_available():
         pytest.skip("oracle/_ref not built")
-    k, m, w, P = 252, 2, 257, 8
+    m, P = 2, 8
+    w = 131 if k == 128 else 257
     g = L.Plan.generate(k * w * 4096 * 2, L.LIBERATION, k, m)
-    assert g.w == 257
+    assert g.w == w
     g.close()
     size = w * P * 2
     data = stripe(k, size, w)
@@ -115,10 +119,12 @@ def test_liberation_w257_encode_vs_reference(cuda):
         p.form_encoding_matrix()
         p.encode_block([data[j] for j in range(k)] + [par[i] for i in range(m)])
         assert np.array_equal(par, ref)
-        sh = np.vstack([data, par])
-        sh[0] = 0
-        assert p.decode_block([sh[i] for i in range(k + m)], [0]) == -1
-        assert "beyond this engine" in L.erasure.last_error()
+        full = np.vstack([data, par])
+        for er in ([5], [k], [k, k + 1], [0, k - 1], [3, k + 1], [k - 1]):
+            sh = full.copy()
+            sh[er] = 0x5A
+            assert p.decode_block([sh[i] for i in range(k + m)], er) == 0, (er, L.erasure.last_error())
+            assert_same(sh, full)
 
 
 # ---------------------------------------------------------------- wide fields (w = 16 / 32)

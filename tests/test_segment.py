@@ -198,3 +198,53 @@ def test_segment_write_iov_matches_reference(cuda, method, k, m, chunk):
             assert np.array_equal(ours, ref), (fracs, errs)
         with pytest.raises(L.ErasureError, match="bytes in the scatter list"):
             p.segment_write_iov([data.reshape(-1)[:-8]], N, chunk)
+
+
+def logical_stream_from_images(img, N, chunk, k, m, n_shift, first):
+    """Undo the LUN placement: the [magic | chunk] stream in logical order that segjerase_write_func
+    hands its LUN child (segment/jerasure.c:1826-1853), from device images (lun.c:1178-1223)."""
+    n, lc = k + m, chunk + 4
+    out = np.empty((N, n, lc), np.uint8)
+    for d in range(n):
+        rows = img[d].reshape(N, lc)
+        for s in range(N):
+            out[s, (d + (first + s) * n_shift) % n] = rows[s]
+    return out.reshape(-1)
+
+
+def gather_iovs(iovs):
+    import ctypes as C
+    return np.concatenate([np.frombuffer((C.c_uint8 * int(ln)).from_address(int(base)), np.uint8).copy()
+                           for base, ln in iovs])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,k,m,chunk", [(L.REED_SOL_VAN, 6, 3, 65536), (L.CAUCHY_GOOD, 6, 3, 16384),
+                                              (L.CAUCHY_GOOD, 10, 4, 65536)])
+def test_segment_encode_iov_is_the_reference_hand_off(cuda, method, k, m, chunk):
+    """lsec_segment_encode_iov: the iovec stream [magic | chunk] x (k+m) per stripe, in logical order,
+    is byte-identical to what the restated segjerase_write_func over the real jerasure hands its LUN
+    child; data iovecs point into the caller's pages (no data copy), parity and magics land in the
+    caller's buffers; straddling stripes and error pages as the reference treats them."""
+    N = 6
+    data = np.stack([stripe(k, chunk, s + 21) for s in range(N)])
+    with L.Plan.for_chunk(method, k, m, chunk) as p:
+        rp = O.RefPlan(method, k, m, 8, p.packet_size)
+        for fracs, errs in SCATTER_CASES:
+            pieces = scatter(data, _cut_points(k, chunk, fracs), errs)
+            iovs, par, mag, keep = p.segment_encode_iov(pieces, N, chunk)
+            assert len(iovs) == 2 * (k + m) * N
+            assert all(ln == (4 if i % 2 == 0 else chunk) for i, (_, ln) in enumerate(iovs))
+            ref = logical_stream_from_images(rp.segment_write_iov(pieces, N, chunk, 1, 0), N, chunk, k, m, 1, 0)
+            assert np.array_equal(gather_iovs(iovs), ref), (fracs, errs)
+            # parity chunk r of stripe s is iovec 2((s(k+m) + k + r)) + 1, inside the caller's parity buffer
+            assert iovs[2 * k + 1][0] == par.ctypes.data and iovs[0][0] == mag.ctypes.data
+        # one piece: every data iovec points into the caller's array, in place
+        flat = np.ascontiguousarray(data.reshape(-1))
+        iovs, par, mag, keep = p.segment_encode_iov([flat], N, chunk)
+        base = flat.ctypes.data
+        for s in range(N):
+            for j in range(k):
+                assert iovs[2 * (s * (k + m) + j) + 1][0] == base + (s * k + j) * chunk
+        with pytest.raises(L.ErasureError, match="bytes in the scatter list"):
+            p.segment_encode_iov([flat[:-8]], N, chunk)

@@ -19,6 +19,7 @@ Then, over the same images, reference harness vs engin
 Outputs (user data, stripe status, bad-device maps) must be identical.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -65,36 +66,63 @@ def main():
     plan = L.Plan.for_chunk(meth, k, m, C)
     rp = O.RefPlan(meth, k, m, 8, plan.packet_size)
 
+    # the depots' buffers: allocated and touched once, reused by every rep (an image allocation
+    # per call would time the kernel's zeroing of fresh pages, for the reference and engine alike)
+    n = k + m
+    ref = np.zeros((n, N * (C + 4)), np.uint8)
+    ours = np.zeros((n, N * (C + 4)), np.uint8)
+    ref.fill(1)
+    ours.fill(1)
+    par = np.ones((N, m, C), np.uint8)
+    mag = np.ones((N, 4), np.uint8)
+    flat = np.ascontiguousarray(data.reshape(-1))
     plan.segment_write(data[:2], a.n_shift, 0)  # warm staging / device images
-    t_ref, t_eng = [], []
+    plan.segment_encode_iov([flat[:2 * k * C]], 2, C)
+    t_ref, t_eng, t_iov = [], [], []
     for _ in range(a.reps):
         t0 = time.perf_counter()
-        ref = rp.segment_write(data, N, C, a.n_shift, 0)
+        rp.segment_write(data, N, C, a.n_shift, 0, out=ref)
         t_ref.append(time.perf_counter() - t0)
         t0 = time.perf_counter()
-        ours = plan.segment_write(data, a.n_shift, 0)
+        plan.segment_write(data, a.n_shift, 0, out=ours)
         t_eng.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        iovs, _, _, keep = plan.segment_encode_iov([flat], N, C, parity=par, magic=mag)
+        t_iov.append(time.perf_counter() - t0)
+    # the iovec stream, placed by the LUN rule, must give the same images
+    stream = np.concatenate([np.frombuffer((ctypes.c_uint8 * int(ln)).from_address(int(b)), np.uint8)
+                             for b, ln in iovs])
+    rec = stream.reshape(N, n, C + 4)
+    placed = np.empty_like(ours)
+    for d in range(n):
+        rows = placed[d].reshape(N, C + 4)
+        for s_ in range(N):
+            rows[s_] = rec[s_, (d + s_ * a.n_shift) % n]
+    iov_identical = bool(np.array_equal(placed, ref))
     identical = bool(np.array_equal(ref, ours))
     t_io_ref = write_depots(ref, a.depot_dir, "c1ref")
     t_io_eng = write_depots(ours, a.depot_dir, "c1eng")
     for tag in ("c1ref", "c1eng"):
         for i in range(k + m):
             os.remove(os.path.join(a.depot_dir, f"{tag}_depot{i}.bin"))
-    tr, te = min(t_ref), min(t_eng)
+    tr, te, ti = min(t_ref), min(t_eng), min(t_iov)
     paths = verify_paths(plan, rp, ours, N, C, k, m, a.n_shift, a.reps) if identical else {}
     print(json.dumps({
         "config": "c1", "workload": f"{a.method}({k}+{m}) segment write, {N} stripes x C={C} B, n_shift={a.n_shift}",
         "images_identical": identical,
         "reference_cpu_gibps": round(gib / tr, 3), "reference_cores": 1,
         "engine_gibps": round(gib / te, 3),
+        "engine_iov_gibps": round(gib / ti, 3), "iov_stream_identical": iov_identical,
         "reference_with_depot_files_gibps": round(gib / (tr + t_io_ref), 3),
         "engine_with_depot_files_gibps": round(gib / (te + t_io_eng), 3),
         "depot_dir": a.depot_dir,
-        "note": "reference = segjerase_write_func loop over real jerasure + zlib (oracle/_ref); engine = "
-                "lsec_segment_write (GPU parity + magic, host memory in/out, PCIe included)",
+        "note": "reference = segjerase_write_func loop over real jerasure + zlib (oracle/_ref), into depot "
+                "images; engine = lsec_segment_write into the same images (GPU parity + magic, host memory in/out, "
+                "PCIe included); engine_iov = lsec_segment_encode_iov, the reference's own hand-off (parity + magic "
+                "on the GPU, iovecs into the user data, no image copies); images preallocated for all three",
         "read_inspect": paths,
     }), flush=True)
-    if not identical or not all(v.get("identical") for v in paths.values()):
+    if not identical or not iov_identical or not all(v.get("identical") for v in paths.values()):
         sys.exit(1)
 
 
