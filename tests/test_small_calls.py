@@ -181,13 +181,16 @@ STRESS = os.path.join(ROOT, "tools", "reg_stress.py")
     ["--method", "cauchy_good", "--k", "6", "--m", "3", "--chunk", "65536", "--stripes", "1"],
     ["--k", "6", "--m", "3", "--chunk", "1048576", "--stripes", "4"],
     ["--method", "cauchy_good", "--k", "6", "--m", "3", "--chunk", "65536", "--stripes", "2", "--pinned"],
+    ["--method", "cauchy_good", "--k", "6", "--m", "3", "--chunk", "65536", "--stripes", "1", "--caller-registered"],
+    ["--k", "6", "--m", "3", "--chunk", "65536", "--stripes", "8", "--caller-registered"],
 ])
 def test_host_calls_under_memory_churn(cuda, args):
     """Host calls while the process frees and reallocates host memory between them (virtual
     ranges and physical pages recycled; tools/reg_stress.py --churn), with stripe-server calls in
     between: the zero-copy slots and server, the in-place-pinned DMA pipeline (36 MiB batches) and
-    caller page-locked buffers reallocated every call.  Every call's bytes are checked against the
-    oracle restatement.  (Kernels over per-call registrations of pageable pages failed exactly this,
+    caller page-locked buffers reallocated every call, and caller-registered buffers (the caller
+    hipHostRegister's each iteration's stripes and unregisters them after, as an allocator that pins
+    its arenas).  Every call's bytes are checked against the oracle restatement.  (Kernels over per-call registrations of pageable pages failed exactly this,
     which is why no route uses them: DESIGN.md §1.)"""
     out = subprocess.run([sys.executable, STRESS, "--seconds", "5", "--churn", "--small-mix", *args],
                          capture_output=True, text=True, timeout=110)
@@ -216,6 +219,8 @@ for C in (65536, 1 << 20):
         assert hip.hipHostUnregister(ctypes.c_void_p(junk.ctypes.data)) != 0
         p.encode_block([d[j] for j in range(9)])
         assert np.array_equal(d[6:], O.encode(L.CAUCHY_GOOD, d[:6], 3, p.packet_size)), C
+        # ... and the caller's error is still there for the caller to read
+        assert hip.hipGetLastError() != 0, C
 print("ok")
 """
 
@@ -223,10 +228,12 @@ print("ok")
 @pytest.mark.gpu
 def test_stale_caller_hip_error_is_not_taken_for_a_launch_failure(cuda):
     """A HIP error the caller's own calls left pending (HIP keeps the last error per thread until
-    it is read) must not fail the engine's next launch: public entry points clear it first
-    (ec_engine.cpp drop_stale_error).  Before that, tools/reg_stress.py --caller-registered saw a
-    1 MiB call fail with the caller's hipHostUnregister error and take the direct-copy retry.
-    Served (64 KiB) and own-launch (1 MiB, 9 MiB per call) stripes, bit-exact, with no retry."""
+    it is read) must neither fail the engine's next launch nor be consumed by it: launches report
+    hipLaunchKernel's own status (lsec::launch_kernel), and the engine never reads the last error
+    to learn about them.  (Round 3 saw tools/reg_stress.py --caller-registered fail a 1 MiB call
+    with the caller's hipHostUnregister error; its fix, clearing the error at every entry point,
+    hid the caller's error from the caller: ADVICE r03.)  Served (64 KiB) and own-launch (1 MiB,
+    9 MiB per call) stripes, bit-exact, with no retry, and the caller's error still pending."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, "-c", STALE_ERROR_SCRIPT, root], capture_output=True, text=True,
                          timeout=110)
