@@ -1,0 +1,301 @@
+// ec_pinning.cpp -- what kind of host memory a call hands over: runtime pointer queries (with a
+// per-call memo), caller page-locked buffers (DMA in place; kernel transport for small runs of
+// hipHostMalloc memory), and pageable batches pinned in place for DMA (InPlacePin).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdarg>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ec_engine.h"
+
+namespace lsec {
+namespace eng {
+
+std::atomic<unsigned long long> g_st_queries{0};  // runtime pointer queries (LSEC_STATS)
+
+thread_local int tl_memo_depth = 0;
+thread_local std::vector<std::pair<const void *, PtrInfo>> tl_memo;
+
+PtrInfo query_ptr(const void *ptr) {
+  if (tl_memo_depth > 0)
+    for (const auto &kv : tl_memo)
+      if (kv.first == ptr) return kv.second;
+  PtrInfo r;
+  hipPointerAttribute_t attr;
+  g_st_queries.fetch_add(1, std::memory_order_relaxed);
+  if (hipPointerGetAttributes(&attr, ptr) == hipSuccess) {
+    r.ok = true;
+    r.type = attr.type;
+    r.dev = attr.devicePointer;
+  } else {
+    (void)hipGetLastError();  // pageable host memory reports an error on some runtimes
+  }
+  if (tl_memo_depth > 0 && tl_memo.size() < 64) tl_memo.push_back({ptr, r});  // small: scanned linearly
+  return r;
+}
+
+// Caller buffers that are already page-locked (hipHostMalloc'd, or hipHostRegister'ed by an
+// allocator that pins its cache pages) need no packing: the DMA engines copy straight
+// between them and the device slots, and the host copy pool stays idle.
+bool is_pinned_host(const void *ptr) {
+  const PtrInfo i = query_ptr(ptr);
+  return i.ok && i.type == hipMemoryTypeHost;
+}
+
+// every staged shard of the first and last stripe pinned?  (a stray pageable pointer in
+// between stays correct -- hipMemcpyAsync accepts pageable memory too, only slower)
+// Ranges pinned in place by a running call (InPlacePin), page-rounded.  Another call that
+// touches them must not take them for caller-pinned memory: the owner unregisters them when
+// it returns, maybe while the other call's DMA is still queued.
+std::mutex g_inplace_mu;
+std::vector<std::pair<uintptr_t, uintptr_t>> g_inplace;
+
+
+bool inplace_overlaps_locked(uintptr_t lo, uintptr_t hi) {
+  for (const auto &r : g_inplace)
+    if (lo < r.second && r.first < hi) return true;
+  return false;
+}
+
+// p..p+len inside one page-locked allocation with a device alias?  (its device address in *dev)
+bool pinned_chunk(const char *p, size_t len, std::vector<PinnedAlloc> &seen, uint64_t *dev) {
+  const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+  for (const PinnedAlloc &a : seen)
+    if (u >= a.lo && u + len <= a.hi) {
+      *dev = static_cast<uint64_t>(static_cast<intptr_t>(u) + a.delta);
+      return true;
+    }
+  const PtrInfo i = query_ptr(p);
+  if (!i.ok || i.type != hipMemoryTypeHost || !i.dev) return false;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(const_cast<char *>(p))) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(base), hi = lo + size;
+  if (u < lo || u + len > hi) return false;
+  const intptr_t delta = reinterpret_cast<intptr_t>(i.dev) - static_cast<intptr_t>(u);
+  seen.push_back({lo, hi, delta});
+  *dev = reinterpret_cast<uint64_t>(i.dev);
+  return true;
+}
+
+bool caller_pinned_aliases(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids,
+                           const std::vector<int> &out_ids, long long C, std::vector<PinnedAlloc> &seen,
+                           std::vector<uint64_t> &dev);
+
+CallerPinned caller_pinned(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
+                           long long C, bool kernel_ok) {
+  CallerPinned r;
+  // A first chunk that is not page-locked settles it, with no lock: every path below returns
+  // "not pinned" for it too, and taking memory for pageable is always safe.  (Per-stripe calls
+  // from hundreds of threads queued on this mutex.)
+  if (nstripes >= 1 && tl_memo_depth > 0)
+    for (const auto &kv : tl_memo)  // a chunk of this call already known not to be page-locked
+      if (!kv.second.ok || kv.second.type != hipMemoryTypeHost)
+        for (const std::vector<int> *ids : {&in_ids, &out_ids})
+          for (int id : *ids)
+            if (ptrs[id] == kv.first) return r;
+  if (!in_ids.empty() && nstripes >= 1 && !is_pinned_host(ptrs[in_ids[0]])) return r;
+  std::lock_guard<std::mutex> lk(g_inplace_mu);
+  if (!g_inplace.empty()) {
+    for (int s = 0; s < nstripes; ++s)
+      for (const std::vector<int> *ids : {&in_ids, &out_ids})
+        for (int id : *ids) {
+          const uintptr_t a = reinterpret_cast<uintptr_t>(ptrs[static_cast<size_t>(s) * km + id]);
+          if (inplace_overlaps_locked(a & ~(kPage - 1), (a + static_cast<uintptr_t>(C) + kPage - 1) & ~(kPage - 1))) return r;
+        }
+  }
+  std::vector<PinnedAlloc> seen;
+  uint64_t d = 0;
+  for (int s : {0, nstripes - 1}) {
+    for (int id : in_ids)
+      if (!pinned_chunk(ptrs[static_cast<size_t>(s) * km + id], static_cast<size_t>(C), seen, &d)) return r;
+    for (int id : out_ids)
+      if (!pinned_chunk(ptrs[static_cast<size_t>(s) * km + id], static_cast<size_t>(C), seen, &d)) return r;
+  }
+  r.pinned = true;
+  r.by_kernel = kernel_ok && caller_pinned_aliases(ptrs, nstripes, km, in_ids, out_ids, C, seen, r.dev);
+  return r;
+}
+
+bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
+         long long C) {
+  if (!routes().pin_in_place) return false;
+  std::vector<std::pair<char *, char *>> pieces;
+  pieces.reserve(static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()));
+  for (int s = 0; s < nstripes; ++s) {
+    for (int id : in_ids) pieces.push_back({ptrs[static_cast<size_t>(s) * km + id], ptrs[static_cast<size_t>(s) * km + id] + C});
+    for (int id : out_ids) pieces.push_back({ptrs[static_cast<size_t>(s) * km + id], ptrs[static_cast<size_t>(s) * km + id] + C});
+  }
+  std::sort(pieces.begin(), pieces.end());
+  std::vector<std::pair<char *, char *>> regions;
+  for (const auto &pc : pieces) {
+    if (!regions.empty() && pc.first < regions.back().second) return false;  // overlapping chunks
+    if (!regions.empty() && pc.first == regions.back().second)
+      regions.back().second = pc.second;
+    else
+      regions.push_back(pc);
+    if (regions.size() > kMaxRegions) return false;
+  }
+  size_t total = 0;
+  for (const auto &r : regions) total += static_cast<size_t>(r.second - r.first);
+  if (total < routes().pin_min_bytes) return false;  // packing a small batch is cheaper than the syscalls
+  // Each DMA from registered pageable memory has a fixed cost on top of the bytes, so pin
+  // only when the copies the pinned path will issue (one per run of host-contiguous chunks,
+  // stripe by stripe) average >= 2.5 MiB; smaller runs pack faster.  Round 1's 4 MiB had
+  // every single-erasure decode below C = 2 MiB packing (RS(6+3) 1 MiB decode: 3.5 MiB runs,
+  // 31 GiB/s packed, 37-46 pinned).  An in-process A/B (tools/pin_run_ab.py,
+  // profiles/r02_v27_pin_run_ab.jsonl) put the break-even near 800 KiB, but the c5 sweep
+  // with that threshold (r02_v38_sweep_c5.jsonl vs r02_v25) lost up to half the rate at
+  // 1.5-2.25 MiB runs (RS(6+3) 256 KiB encode 32 -> 16, 512 KiB 29 -> 22.5) while runs of
+  // 2.75 MiB and up gained (RS(10+4) 512 KiB decode 30 -> 40).
+  size_t runs = 0;
+  for (const std::vector<int> *ids : {&in_ids, &out_ids}) {
+    const char *end = nullptr;
+    for (int s = 0; s < nstripes; ++s)
+      for (int id : *ids) {
+        const char *b = ptrs[static_cast<size_t>(s) * km + id];
+        if (b != end) ++runs;
+        end = b + C;
+      }
+  }
+  if (runs == 0) return false;
+  if (total / runs < routes().pin_min_run) return false;
+  {
+    // claim the page-rounded regions, so a concurrent call over the same pages packs
+    std::lock_guard<std::mutex> lk(g_inplace_mu);
+    for (const auto &r : regions) {
+      const uintptr_t lo = reinterpret_cast<uintptr_t>(r.first) & ~(kPage - 1);
+      const uintptr_t hi = (reinterpret_cast<uintptr_t>(r.second) + kPage - 1) & ~(kPage - 1);
+      if (inplace_overlaps_locked(lo, hi)) {
+        claimed_.clear();
+        return false;
+      }
+      claimed_.push_back({lo, hi});
+    }
+    for (size_t i = 1; i < claimed_.size(); ++i)
+      if (claimed_[i].first < claimed_[i - 1].second) {  // two (sorted) regions share a page
+        claimed_.clear();
+        return false;
+      }
+    g_inplace.insert(g_inplace.end(), claimed_.begin(), claimed_.end());
+  }
+  // whole pages (the claims above are page-rounded and disjoint)
+  for (const auto &r : regions) {
+    char *lo = reinterpret_cast<char *>(reinterpret_cast<uintptr_t>(r.first) & ~(kPage - 1));
+    char *hi = reinterpret_cast<char *>((reinterpret_cast<uintptr_t>(r.second) + kPage - 1) & ~(kPage - 1));
+    if (hipHostRegister(lo, static_cast<size_t>(hi - lo), hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
+      (void)hipGetLastError();
+      release();
+      return false;
+    }
+    held_.push_back(lo);
+  }
+  return true;
+}
+
+void InPlacePin::release() {
+  for (char *b : held_)
+    if (hipHostUnregister(b) != hipSuccess) {
+      (void)hipGetLastError();
+      static std::atomic<bool> told{false};
+      if (!told.exchange(true)) fprintf(stderr, "liblstore_ec: hipHostUnregister(%p) failed\n", static_cast<void *>(b));
+    }
+  held_.clear();
+  if (claimed_.empty()) return;
+  std::lock_guard<std::mutex> lk(g_inplace_mu);
+  for (const auto &c : claimed_) {
+    auto it = std::find(g_inplace.begin(), g_inplace.end(), c);
+    if (it != g_inplace.end()) g_inplace.erase(it);
+  }
+  claimed_.clear();
+}
+
+void add_run(std::vector<DmaRun> &v, char *dst, const char *src, size_t n) {
+  if (!v.empty() && v.back().dst + v.back().bytes == dst && v.back().src + v.back().bytes == src)
+    v.back().bytes += n;
+  else
+    v.push_back({dst, src, n});
+}
+
+// kernel transport pieces of one chunk (addresses already device-visible)
+// (returns 0 when either address is 0 -- a host byte outside the pinned regions -- so the
+// caller stops before launching)
+size_t add_pieces(lsec::CopyPiece *pl, size_t n, uint64_t src, uint64_t dst, size_t len) {
+  if (src == 0 || dst == 0) return 0;
+  for (size_t o = 0; o < len; o += lsec::kPieceBytes) pl[n++] = {src + o, dst + o, std::min<uint64_t>(lsec::kPieceBytes, len - o)};
+  return n;
+}
+
+KernelCopy kernel_copy_policy() { return routes().kernel_copy ? KernelCopy::kCallerPinned : KernelCopy::kNever; }
+
+// every transferred chunk (and column block) 16-byte aligned, as the copy-piece kernel needs
+bool kernel_transport_aligned(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids,
+                              const std::vector<int> &out_ids, long long C, long long cb) {
+  if (C % 16 != 0 || cb % 16 != 0) return false;
+  for (int s = 0; s < nstripes; ++s)
+    for (const std::vector<int> *ids : {&in_ids, &out_ids})
+      for (int id : *ids)
+        if (reinterpret_cast<uintptr_t>(ptrs[static_cast<size_t>(s) * km + id]) % 16 != 0) return false;
+  return true;
+}
+
+// Caller page-locked buffers with small runs (average < 1 MiB: DMA of 384 KiB runs from
+// hipHostMalloc memory moves ~20 GiB/s, profiles/r01_v27_kernel_copy_ab.txt) move by kernel,
+// once EVERY chunk is checked: page-locked, inside one allocation, with a device address
+// (a pageable chunk between pinned ones is harmless to a DMA but would fault a kernel).  The
+// check costs ~0.06 us per chunk (tools/probes/pinned_attr_probe.cpp).  dev[i] gets the device
+// address of chunk i, in the order stripe, then in_ids, then out_ids.
+// (called by caller_pinned with g_inplace_mu held)
+bool caller_pinned_aliases(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids,
+                           const std::vector<int> &out_ids, long long C, std::vector<PinnedAlloc> &seen,
+                           std::vector<uint64_t> &dev) {
+  size_t runs = 0, total = 0;
+  for (const std::vector<int> *ids : {&in_ids, &out_ids}) {
+    const char *end = nullptr;
+    for (int s = 0; s < nstripes; ++s)
+      for (int id : *ids) {
+        const char *b = ptrs[static_cast<size_t>(s) * km + id];
+        if (b != end) ++runs;
+        end = b + C;
+        total += static_cast<size_t>(C);
+      }
+  }
+  if (runs == 0 || total / runs >= routes().kernel_copy_max_run) return false;
+  dev.clear();
+  dev.reserve(static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()));
+  for (int s = 0; s < nstripes; ++s)
+    for (const std::vector<int> *ids : {&in_ids, &out_ids})
+      for (int id : *ids) {
+        uint64_t d = 0;
+        if (!pinned_chunk(ptrs[static_cast<size_t>(s) * km + id], static_cast<size_t>(C), seen, &d)) return false;
+        dev.push_back(d);
+      }
+  return true;
+}
+
+void split_pieces(std::vector<lsec::CopyPiece> &v, uint64_t src, uint64_t dst, size_t len) {
+  for (size_t o = 0; o < len; o += lsec::kPieceBytes) v.push_back({src + o, dst + o, std::min<uint64_t>(lsec::kPieceBytes, len - o)});
+}
+
+hipError_t issue_runs(const std::vector<DmaRun> &v, hipMemcpyKind kind, hipStream_t st) {
+  for (const DmaRun &r : v) {
+    const hipError_t e = hipMemcpyAsync(r.dst, r.src, r.bytes, kind, st);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace eng
+}  // namespace lsec
