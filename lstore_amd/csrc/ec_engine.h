@@ -230,6 +230,7 @@ bool inplace_overlaps_locked(uintptr_t lo, uintptr_t hi);
 struct PinnedAlloc {
   uintptr_t lo, hi;
   intptr_t delta;
+  bool kernel_ok;  // a hipHostMalloc allocation: GPU kernels may read and write it in place
 };
 
 struct CallerPinned {

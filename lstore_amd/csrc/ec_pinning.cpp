@@ -66,12 +66,31 @@ bool inplace_overlaps_locked(uintptr_t lo, uintptr_t hi) {
   return false;
 }
 
-// p..p+len inside one page-locked allocation with a device alias?  (its device address in *dev)
-bool pinned_chunk(const char *p, size_t len, std::vector<PinnedAlloc> &seen, uint64_t *dev) {
+// Which caller page-locked memory a GPU kernel may touch in place.  Kernels read and write
+// hipHostMalloc allocations in place (the stripe server's direct parts, the copy-piece kernel,
+// a zero-copy launch over caller chunks); ranges the caller pinned with hipHostRegister move by
+// DMA only.  Round 3 found that kernels over per-call registrations of pageable memory return
+// stale bytes once the process recycles host memory (profiles/r03_v16_reg_repro.jsonl), while
+// DMA over the same registrations stays exact (r03_v18_churn_default_routes.jsonl).  A caller's
+// own registration of its arenas is the same mechanism, and what separates the two could not be
+// named from the records, so registered memory gets the transport shown safe.
+// hipHostMalloc memory answers hipHostGetFlags; a hipHostRegister'ed range does not
+// (profiles/r04_alloc_kind_probe.jsonl).
+bool kernel_visible_allocation(const char *p) {
+  unsigned flags = 0;
+  if (hipHostGetFlags(&flags, const_cast<char *>(p)) == hipSuccess) return true;
+  (void)hipGetLastError();
+  return false;
+}
+
+// p..p+len inside one page-locked allocation with a device alias?  (its device address in *dev;
+// *kernel_ok: the allocation is one kernels may touch in place)
+bool pinned_chunk(const char *p, size_t len, std::vector<PinnedAlloc> &seen, uint64_t *dev, bool *kernel_ok) {
   const uintptr_t u = reinterpret_cast<uintptr_t>(p);
   for (const PinnedAlloc &a : seen)
     if (u >= a.lo && u + len <= a.hi) {
       *dev = static_cast<uint64_t>(static_cast<intptr_t>(u) + a.delta);
+      if (kernel_ok) *kernel_ok = a.kernel_ok;
       return true;
     }
   const PtrInfo i = query_ptr(p);
@@ -85,8 +104,10 @@ bool pinned_chunk(const char *p, size_t len, std::vector<PinnedAlloc> &seen, uin
   const uintptr_t lo = reinterpret_cast<uintptr_t>(base), hi = lo + size;
   if (u < lo || u + len > hi) return false;
   const intptr_t delta = reinterpret_cast<intptr_t>(i.dev) - static_cast<intptr_t>(u);
-  seen.push_back({lo, hi, delta});
+  const bool kok = kernel_visible_allocation(p);
+  seen.push_back({lo, hi, delta, kok});
   *dev = reinterpret_cast<uint64_t>(i.dev);
+  if (kernel_ok) *kernel_ok = kok;
   return true;
 }
 
@@ -120,9 +141,9 @@ CallerPinned caller_pinned(char **ptrs, int nstripes, int km, const std::vector<
   uint64_t d = 0;
   for (int s : {0, nstripes - 1}) {
     for (int id : in_ids)
-      if (!pinned_chunk(ptrs[static_cast<size_t>(s) * km + id], static_cast<size_t>(C), seen, &d)) return r;
+      if (!pinned_chunk(ptrs[static_cast<size_t>(s) * km + id], static_cast<size_t>(C), seen, &d, nullptr)) return r;
     for (int id : out_ids)
-      if (!pinned_chunk(ptrs[static_cast<size_t>(s) * km + id], static_cast<size_t>(C), seen, &d)) return r;
+      if (!pinned_chunk(ptrs[static_cast<size_t>(s) * km + id], static_cast<size_t>(C), seen, &d, nullptr)) return r;
   }
   r.pinned = true;
   r.by_kernel = kernel_ok && caller_pinned_aliases(ptrs, nstripes, km, in_ids, out_ids, C, seen, r.dev);
@@ -279,7 +300,8 @@ bool caller_pinned_aliases(char **ptrs, int nstripes, int km, const std::vector<
     for (const std::vector<int> *ids : {&in_ids, &out_ids})
       for (int id : *ids) {
         uint64_t d = 0;
-        if (!pinned_chunk(ptrs[static_cast<size_t>(s) * km + id], static_cast<size_t>(C), seen, &d)) return false;
+        bool kok = false;
+        if (!pinned_chunk(ptrs[static_cast<size_t>(s) * km + id], static_cast<size_t>(C), seen, &d, &kok) || !kok) return false;
         dev.push_back(d);
       }
   return true;
