@@ -143,13 +143,18 @@ struct RouteTable {
   // route choice by a call's bytes (inputs + outputs)
   size_t zerocopy_max;         // LSEC_ZEROCOPY_KB = 4096: up to here, routes 1-2 (server, own slot)
   size_t coalesce_max;         // LSEC_COALESCE_MB = 16: up to here, route 3 (dispatcher)
-  size_t own_pipeline_min;     // 4 MiB: from here to coalesce_max, a call's own pipeline ...
+  size_t own_pipeline_min;     // LSEC_OWN_PIPELINE_MIN_KB = 4096: from here to coalesce_max, a call's own pipeline ...
   int own_pipeline_max;        // LSEC_OWN_PIPELINE_MAX = max(2, cpus / 2): ... while this few run
   bool own_pipeline_slot;      // LSEC_ZC_BIG = 1: that pipeline is the own slot (route 2), else route 4
+  int own_dma_max;             // LSEC_OWN_DMA_MAX = 2: while at most this many own pipelines run, each
+                               // takes route 4 pinned in place (DMA, no packing) ...
+  size_t own_dma_min_bytes;    // 1 MiB: ... when the call has this many bytes ...
+  size_t own_dma_min_run;      // LSEC_OWN_DMA_MIN_RUN_KB = 1024: ... and its DMA runs average this
   bool server;                 // LSEC_SERVER = 1: route 1 on
+  size_t srv_nt_min;           // LSEC_SRV_NT_MIN_KB (off): server calls copying this much in use streaming stores
   // transports
   bool pin_in_place;           // LSEC_NO_HOST_REGISTER unset: pageable batches may be pinned in place for DMA
-  size_t pin_min_bytes;        // 8 MiB: ... when the batch has at least this many bytes
+  size_t pin_min_bytes;        // LSEC_PIN_MIN_KB = 8192: ... when the batch has at least this many bytes
   size_t pin_min_run;          // LSEC_PIN_MIN_RUN_KB = 2560: ... and its DMA copies average this run
   bool kernel_copy;            // LSEC_KERNEL_COPY != 0: hipHostMalloc'd caller runs may move by kernel
   size_t kernel_copy_max_run;  // 1 MiB: ... when their runs average less
@@ -265,8 +270,10 @@ class InPlacePin {
   // caller had since reused, once host arrays were freed and reallocated between calls;
   // tools/reg_stress.py --churn, profiles/r03_v16_reg_repro.jsonl.  DMA over the same
   // registrations stayed exact: r03_v18_churn_default_routes.jsonl.)
+  // min_bytes / min_run: the batch's smallest total and average DMA run worth pinning
+  // (RouteTable pin_min_* for batches, own_dma_min_* for a lone call's own pipeline)
   bool pin(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
-           long long C);
+           long long C, size_t min_bytes, size_t min_run);
   void release();
 
  private:
@@ -303,8 +310,11 @@ bool kernel_transport_aligned(char **ptrs, int nstripes, int km, const std::vect
 
 // ---------------------------------------------------------------- routes
 // route 4, the call's own staging pipeline (ec_staging.cpp); magic_host: stripe magics too
+// eager_pin: pin pageable chunks in place at the lower own_dma_min_* thresholds (a lone call's own
+// pipeline, route_host), else at pin_min_*
 int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
-             const std::vector<int> &out_ids, const void *cells, int kind, uint8_t *magic_host = nullptr);
+             const std::vector<int> &out_ids, const void *cells, int kind, uint8_t *magic_host = nullptr,
+             bool eager_pin = false);
 hipError_t launch_magic_groups(lsec::MagicArgs ma, const ShardRef *sh, int km, hipStream_t st);
 // route 3, the device's dispatcher (ec_dispatch.cpp)
 int run_coalesced(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,

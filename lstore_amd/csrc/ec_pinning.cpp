@@ -151,7 +151,7 @@ CallerPinned caller_pinned(char **ptrs, int nstripes, int km, const std::vector<
 }
 
 bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
-         long long C) {
+                     long long C, size_t min_bytes, size_t min_run) {
   if (!routes().pin_in_place) return false;
   std::vector<std::pair<char *, char *>> pieces;
   pieces.reserve(static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()));
@@ -171,7 +171,7 @@ bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &
   }
   size_t total = 0;
   for (const auto &r : regions) total += static_cast<size_t>(r.second - r.first);
-  if (total < routes().pin_min_bytes) return false;  // packing a small batch is cheaper than the syscalls
+  if (total < min_bytes) return false;  // packing a small batch is cheaper than the syscalls
   // Each DMA from registered pageable memory has a fixed cost on top of the bytes, so pin
   // only when the copies the pinned path will issue (one per run of host-contiguous chunks,
   // stripe by stripe) average >= 2.5 MiB; smaller runs pack faster.  Round 1's 4 MiB had
@@ -192,7 +192,7 @@ bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &
       }
   }
   if (runs == 0) return false;
-  if (total / runs < routes().pin_min_run) return false;
+  if (total / runs < min_run) return false;
   {
     // claim the page-rounded regions, so a concurrent call over the same pages packs
     std::lock_guard<std::mutex> lk(g_inplace_mu);

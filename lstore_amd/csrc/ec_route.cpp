@@ -15,6 +15,7 @@
 #include <thread>
 #include <vector>
 
+#include <cstdint>
 #include <cstdio>
 
 #include "ec_host.h"
@@ -35,12 +36,16 @@ const RouteTable &routes() {
     r.cpus = usable_cpus();
     r.zerocopy_max = static_cast<size_t>(std::max(0L, env("LSEC_ZEROCOPY_KB", 4096))) << 10;
     r.coalesce_max = static_cast<size_t>(std::max(0L, env("LSEC_COALESCE_MB", 16))) << 20;
-    r.own_pipeline_min = 4u << 20;
+    r.own_pipeline_min = static_cast<size_t>(std::max(0L, env("LSEC_OWN_PIPELINE_MIN_KB", 4096))) << 10;
     r.own_pipeline_max = static_cast<int>(std::max(0L, env("LSEC_OWN_PIPELINE_MAX", std::max(2, r.cpus / 2))));
     r.own_pipeline_slot = env("LSEC_ZC_BIG", 1) != 0;
+    r.own_dma_max = static_cast<int>(std::max(0L, env("LSEC_OWN_DMA_MAX", 2)));
+    r.own_dma_min_bytes = 1u << 20;
+    r.own_dma_min_run = static_cast<size_t>(std::max(0L, env("LSEC_OWN_DMA_MIN_RUN_KB", 1024))) << 10;
     r.server = env("LSEC_SERVER", 1) != 0;
+    r.srv_nt_min = env("LSEC_SRV_NT_MIN_KB", -1) < 0 ? SIZE_MAX : static_cast<size_t>(env("LSEC_SRV_NT_MIN_KB", 0)) << 10;
     r.pin_in_place = getenv("LSEC_NO_HOST_REGISTER") == nullptr;
-    r.pin_min_bytes = 8u << 20;
+    r.pin_min_bytes = static_cast<size_t>(std::max(0L, env("LSEC_PIN_MIN_KB", 8192))) << 10;
     r.pin_min_run = static_cast<size_t>(std::max(0L, env("LSEC_PIN_MIN_RUN_KB", 2560))) << 10;
     r.kernel_copy = env("LSEC_KERNEL_COPY", 1) != 0;
     r.kernel_copy_max_run = 1u << 20;
@@ -124,10 +129,12 @@ hipStream_t thread_stream() {
 // call's bytes B (inputs + outputs):
 //   B <= zerocopy_max (4 MiB)        route 1, the stripe server (one stripe it can serve), else
 //                                    route 2, this thread's own page-locked slot (zero-copy launch)
-//   B <= coalesce_max (16 MiB)       from own_pipeline_min (4 MiB), while fewer than
-//                                    own_pipeline_max such calls run: route 2 (own slot), else
-//                                    route 4 (own staging pipeline); otherwise route 3, the
-//                                    device's dispatcher (coalesced with concurrent calls)
+//   B <= coalesce_max (16 MiB)       from own_pipeline_min (4 MiB), while at most
+//                                    own_pipeline_max such calls run, the call's own pipeline:
+//                                    while at most own_dma_max run, route 4 pinned in place at the
+//                                    lower own_dma_min_* thresholds (DMA, no packing), else route 2
+//                                    (own slot); beyond own_pipeline_max, route 3, the device's
+//                                    dispatcher (coalesced with concurrent calls)
 //   larger                           route 4, the call's own staging pipeline (pinned in place
 //                                    for DMA when pin_min_bytes / pin_min_run allow, else packed)
 // Route 2 answers 1 when its slot would pass the device's page-locked budget; the call then
@@ -147,9 +154,18 @@ int route_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::ve
   }
   if (bytes > rt.coalesce_max) return run_host(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
   if (bytes >= rt.own_pipeline_min && rt.own_pipeline_max > 0) {
-    if (own_inflight.fetch_add(1, std::memory_order_acq_rel) < rt.own_pipeline_max) {
-      int rc = rt.own_pipeline_slot ? run_zerocopy(e, ptrs, nstripes, C, in_ids, out_ids, image, kind) : 1;
-      if (rc == 1) rc = run_host(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
+    const int running = own_inflight.fetch_add(1, std::memory_order_acq_rel) + 1;
+    if (running <= rt.own_pipeline_max) {
+      int rc;
+      if (running <= rt.own_dma_max) {
+        // few running: pinned in place and DMA'd, no packing (1 MiB Cauchy(6+3) decodes at one
+        // thread 22.5 -> 31.5 GiB/s, the reference 29.4; level at two, 37.3 / 37.1;
+        // profiles/r04_v3_fnptr_dma_ab.jsonl)
+        rc = run_host(e, ptrs, nstripes, C, in_ids, out_ids, image, kind, nullptr, true);
+      } else {
+        rc = rt.own_pipeline_slot ? run_zerocopy(e, ptrs, nstripes, C, in_ids, out_ids, image, kind) : 1;
+        if (rc == 1) rc = run_host(e, ptrs, nstripes, C, in_ids, out_ids, image, kind);
+      }
       own_inflight.fetch_sub(1, std::memory_order_acq_rel);
       return rc;
     }

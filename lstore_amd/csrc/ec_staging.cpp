@@ -134,7 +134,7 @@ hipError_t launch_magic_groups(lsec::MagicArgs ma, const ShardRef *sh, int km, h
 // bytewise on any 8-byte boundary, bitsliced on super-packet boundaries -- so a block is a
 // valid independent sub-stripe).
 int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vector<int> &in_ids,
-             const std::vector<int> &out_ids, const void *cells, int kind, uint8_t *magic_host) {
+             const std::vector<int> &out_ids, const void *cells, int kind, uint8_t *magic_host, bool eager_pin) {
   lio_erasure_plan_t *p = &e->pub;
   const int km = p->data_strips + p->parity_strips;
   // staged position of every device id (for the stripe magic, which covers all k+m chunks)
@@ -190,7 +190,10 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   const bool aligned = kpol != KernelCopy::kNever && kernel_transport_aligned(ptrs, nstripes, km, in_ids, out_ids, C, cb);
   CallerPinned cp = caller_pinned(ptrs, nstripes, km, in_ids, out_ids, C, aligned);
   const bool caller_pinned = cp.pinned;
-  const bool pinned = caller_pinned || inplace.pin(ptrs, nstripes, km, in_ids, out_ids, C);
+  const RouteTable &rt = routes();
+  const bool pinned = caller_pinned || inplace.pin(ptrs, nstripes, km, in_ids, out_ids, C,
+                                                   eager_pin ? rt.own_dma_min_bytes : rt.pin_min_bytes,
+                                                   eager_pin ? rt.own_dma_min_run : rt.pin_min_run);
   const std::vector<uint64_t> &calias = cp.dev;  // caller-pinned chunks moved by kernel: their device addresses
   const bool caller_by_kernel = cp.by_kernel;
   const size_t nio = in_ids.size() + out_ids.size();

@@ -14,6 +14,8 @@
 #include <thread>
 #include <vector>
 
+#include <immintrin.h>
+
 #include "ec_server.h"
 #include "ec_engine.h"
 
@@ -126,6 +128,7 @@ class StripeServer {
       }
     }
     uint32_t want[kMaxParts];
+    const bool nt = static_cast<size_t>(C) * nin >= routes().srv_nt_min;
     for (int q = 0; q < nparts; ++q) {
       const int sl = slot[q];
       const long long c0 = static_cast<long long>(q) * len, n = std::min(len, C - c0);
@@ -146,10 +149,12 @@ class StripeServer {
         for (size_t j = 0; j < nin; ++j) {
           // plain stores: for these 4 KiB pieces streaming ones cost 15 -> 18 us p50 at one
           // thread (the server reads them back from DRAM instead of the host's caches;
-          // profiles/r03_v27_fnptr_fair.jsonl)
-          std::memcpy(region + j * n, ptrs[in_ids[j]] + c0, static_cast<size_t>(n));
+          // profiles/r03_v27_fnptr_fair.jsonl); calls of srv_nt_min bytes and more stream
+          if (nt) host_copy(region + j * n, ptrs[in_ids[j]] + c0, static_cast<size_t>(n));
+          else std::memcpy(region + j * n, ptrs[in_ids[j]] + c0, static_cast<size_t>(n));
           d.in[j] = dregion + j * n;
         }
+        if (nt) _mm_sfence();
         for (size_t r = 0; r < nout; ++r) d.out[r] = dregion + (nin + r) * n;
       }
       want[q] = ++seq_[sl] == 0 ? ++seq_[sl] : seq_[sl];
