@@ -1,5 +1,5 @@
 // ec_server.h -- shared layout of the stripe server (ec_server.hip) and its host side
-// (ec_engine.cpp, StripeServer).  Internal to liblstore_ec.
+// (ec_stripe_server.cpp, StripeServer).  Internal to liblstore_ec.
 #pragma once
 
 #include <hip/hip_runtime.h>

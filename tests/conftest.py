@@ -11,7 +11,7 @@ for p in (ROOT, os.path.join(ROOT, "tests")):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs on the GPU box via gpurun)")
-    # an engine abort (ec_engine.cpp fatal) also appends its reason here: pytest's capture of fd 2
+    # an engine abort (ec_plan.cpp fatal) also appends its reason here: pytest's capture of fd 2
     # is lost with an aborting process
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     os.environ.setdefault("LSEC_FATAL_LOG", os.path.join(ROOT, "gpurun_out", "lsec_fatal.log"))

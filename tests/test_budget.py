@@ -1,4 +1,4 @@
-"""CPU test of the zero-copy page-locked accounting (ec_engine.cpp PinnedBudget): each device's
+"""CPU test of the zero-copy page-locked accounting (ec_engine.h PinnedBudget): each device's
 stripe server region (~93 MiB) is accounted apart from the per-thread zero-copy slots, whose
 budget (LSEC_ZC_SLOTS_MB) applies per device -- so with the in-process device set spread over
 8 GPUs (lsec_set_host_devices), a device's threads get the same slot budget as with one GPU

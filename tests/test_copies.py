@@ -1,4 +1,4 @@
-"""CPU tests of the host copies behind packing and unpacking (ec_engine.cpp stream_copy: 16-byte
+"""CPU tests of the host copies behind packing and unpacking (ec_hostcopy.cpp stream_copy: 16-byte
 non-temporal stores after a byte-wise head, memcpy tail; and the copy pool that spreads pieces
 over its workers): random source / destination offsets and lengths against memcpy, with the
 bytes around every destination checked untouched (lsec_selftest_copies), so no GPU is needed."""

@@ -1,4 +1,4 @@
-"""CPU tests of the completion waits behind the per-stripe calls (ec_engine.cpp FlagWaits:
+"""CPU tests of the completion waits behind the per-stripe calls (ec_waits.cpp FlagWaits:
 bounded spinning, lock-free futex parking, poller threads): host threads stand in for the GPU
 and write the flags (lsec_selftest_waits), so no GPU is needed.  Waiters wait on 1..16 flags
 set in random order after 0-300 us, as a call's server parts complete."""

@@ -160,8 +160,7 @@ def main():
         small.close()
     print(json.dumps({"k": k, "m": m, "w": a.w, "chunk": C, "stripes": n, "iters": it, "reuse": a.reuse,
                       "small_mix": a.small_mix, "churn": a.churn, "pinned": a.pinned, "caller_registered": a.caller_registered, "bad_small": bad_small, "server": os.environ.get("LSEC_SERVER", ""),
-                      "fresh_plan": a.fresh_plan, "dev_first": a.dev_first, "reg_zc": os.environ.get("LSEC_REG_ZC", ""),
-                      "reg_flags": os.environ.get("LSEC_REG_FLAGS", ""), "offset": a.offset, "method": a.method, "bad_encode": bad_enc, "bad_decode": bad_dec,
+                      "fresh_plan": a.fresh_plan, "dev_first": a.dev_first, "offset": a.offset, "method": a.method, "bad_encode": bad_enc, "bad_decode": bad_dec,
                       "first_bad": first}), flush=True)
 
 
