@@ -319,30 +319,33 @@ void share_slice_pairs(std::vector<std::vector<int>> &rows, int W, int cap, std:
 
 }  // namespace
 
-int gfw_tile(int w) { return 256 * 4 * w; }
+bool gfw_rowsplit(int w, int R) {
+  // LSEC_JIT_VARIANT bit 19: the wave-pair row split below (w = 32, 3-4 rows)
+  return w == 32 && R >= 3 && ((jit_variant() >> 19) & 1);
+}
 
-std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
-  // LSEC_JIT_VARIANT bits 8-15: most shared pairs per input (0: the default 32, 255: none);
-  // bit 16: let the compiler schedule loads freely (no one-input-ahead prefetch fenced by sched
-  // barriers: it then hoists every input's loads and spills at 10+4, w = 32)
-  const int capv = (jit_variant() >> 8) & 255;
-  const int cap = capv == 0 ? 32 : capv == 255 ? 0 : capv;
-  const bool fenced = !((jit_variant() >> 16) & 1);
-  // bits 17-18: inputs loaded ahead of their use (0: the default 1)
-  const int ahead = std::max(1, (jit_variant() >> 17) & 3);
-  const int tile = gfw_tile(W);  // the launch covers whole tiles only
-  std::ostringstream s;
+bool gfw_ring(int w, int R) {
+  // LSEC_JIT_VARIANT bit 22: the LDS-DMA ring below (not with the row split)
+  return (w == 16 || w == 32) && !gfw_rowsplit(w, R) && ((jit_variant() >> 22) & 1);
+}
+
+int gfw_tile(int w, int R) { return gfw_rowsplit(w, R) ? 128 * 4 * w : 256 * 4 * w; }
+
+namespace {
+
+// Types, the bit transpose and the whole-tile loads / stores shared by both network shapes: a
+// lane's W dwords of a shard are W/4 pieces of 16 B, `stride` bytes apart
+void gfw_prelude(std::ostringstream &s, int R, int K, int W, int stride) {
   s << "typedef unsigned int u32;\n"
        "typedef u32 u32x4 __attribute__((ext_vector_type(4)));\n"
        "typedef u32 u32x2 __attribute__((ext_vector_type(2)));\n"
        "struct Ref { unsigned long long base; long long stride; };\n"
     << "struct Args { long long size; int nstripes; int pad; Ref in[" << K << "]; Ref out[" << R << "]; };\n"
     << "#define W " << W << "\n"
+    << "#define PIECE " << stride << "\n"
        "#define X3(a,b,c) __builtin_amdgcn_bitop3_b32((a),(b),(c),0x96)\n"
        "#define G(a) ((const __attribute__((address_space(1))) u32x4 *)(a))\n"
        "#define GW(a) ((__attribute__((address_space(1))) u32x4 *)(a))\n"
-       "#define G2(a) ((const __attribute__((address_space(1))) u32x2 *)(a))\n"
-       "#define GW2(a) ((__attribute__((address_space(1))) u32x2 *)(a))\n"
        // the W x W bit transpose of k_gfw_transposed (ec_kernels_impl.h, transpose_units)
        "template <int d> __device__ static inline void tb(u32 (&D)[W], u32 m) {\n"
        "#pragma unroll\n"
@@ -360,20 +363,363 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
        "    D[r] = __builtin_amdgcn_perm(y, x, 0x06020400u); D[r + 8] = __builtin_amdgcn_perm(y, x, 0x07030501u); }\n"
        "  tb<4>(D, 0x0F0F0F0Fu); tb<2>(D, 0x33333333u); tb<1>(D, 0x55555555u);\n"
        "}\n"
-       // a lane's W dwords of a shard: W/4 pieces of 16 B, 4 KiB apart.  Whole tiles only: the
-       // launcher hands a ragged tail to the generic kernel, so loads are unconditional and each
-       // tile is one basic block for the scheduler
+       // whole tiles only: the launcher hands a ragged tail to the generic kernel, so loads are
+       // unconditional and each tile is one basic block for the scheduler
        "__device__ static inline void ld(u32 (&e)[W], unsigned long long p) {\n"
        "#pragma unroll\n"
-       "  for (int q = 0; q < W / 4; ++q) { const u32x4 v = __builtin_nontemporal_load(G(p + q * 4096));\n"
+       "  for (int q = 0; q < W / 4; ++q) { const u32x4 v = __builtin_nontemporal_load(G(p + q * PIECE));\n"
        "    e[4 * q] = v.x; e[4 * q + 1] = v.y; e[4 * q + 2] = v.z; e[4 * q + 3] = v.w; }\n"
        "}\n"
        "__device__ static inline void st(const u32 (&h)[W], unsigned long long p) {\n"
        "#pragma unroll\n"
        "  for (int q = 0; q < W / 4; ++q)\n"
-       "    __builtin_nontemporal_store((u32x4){h[4 * q], h[4 * q + 1], h[4 * q + 2], h[4 * q + 3]}, GW(p + q * 4096));\n"
-       "}\n"
+       "    __builtin_nontemporal_store((u32x4){h[4 * q], h[4 * q + 1], h[4 * q + 2], h[4 * q + 3]}, GW(p + q * PIECE));\n"
+       "}\n";
+}
+
+// Input j's contribution to output rows `rows` (accumulators acc[i] of row rows[i]): slice b of
+// row r takes the input slices x (in array `e`, transposed) with bit b of c_rj * x^x set -- the
+// bitmatrix block of the coefficient -- after common-pair elimination over those rows
+void gfw_net(std::ostringstream &s, const uint32_t *mat, int K, int W, int j, const std::vector<int> &rows,
+             const std::vector<std::string> &acc, std::vector<std::vector<bool>> &live, int cap, const std::string &e,
+             const char *ind, int b0 = 0, int b1 = -1) {
+  // output slices b0 .. b1-1 only (accumulator element b - b0)
+  if (b1 < 0) b1 = W;
+  std::vector<std::vector<int>> sl(rows.size() * W);
+  bool any = false;
+  for (size_t i = 0; i < rows.size(); ++i) {
+    uint32_t cx = mat[rows[i] * K + j];
+    any |= cx != 0;
+    for (int x = 0; x < W && cx; ++x) {
+      for (int b = b0; b < b1; ++b)
+        if ((cx >> b) & 1u) sl[i * W + b].push_back(x);
+      cx = gfw_times_x(cx, W);
+    }
+  }
+  if (!any) return;
+  std::vector<std::pair<int, int>> pairs;
+  if (cap > 0) share_slice_pairs(sl, W, cap, pairs);
+  // LSEC_JIT_VARIANT bit 21: serial folds (below) instead of balanced 3-input XOR trees
+  const bool linear = (jit_variant() >> 21) & 1;
+  auto nm = [&](int x) { return x < W ? e + "[" + std::to_string(x) + "]" : "p" + std::to_string(x - W); };
+  s << ind << "{\n";
+  for (size_t i = 0; i < pairs.size(); ++i)
+    s << ind << "  const u32 p" << i << " = " << nm(pairs[i].first) << " ^ " << nm(pairs[i].second) << ";\n";
+  for (size_t i = 0; i < rows.size(); ++i)
+    for (int b = b0; b < b1; ++b) {
+      const auto &row = sl[i * W + b];
+      if (row.empty()) continue;
+      std::vector<std::string> t;
+      const std::string a = acc[i] + "[" + std::to_string(b - b0) + "]";
+      if (live[i][b - b0]) t.push_back(a);
+      for (int x : row) t.push_back(nm(x));
+      if (linear) {
+        // a serial fold into the accumulator: no partial sums of the inputs alone for the
+        // scheduler to hoist (each is a VGPR live until its fold)
+        std::string v = t[0];
+        size_t k = 1;
+        for (; k + 2 <= t.size(); k += 2) {
+          s << ind << "  " << a << " = X3(" << v << ", " << t[k] << ", " << t[k + 1] << ");\n";
+          v = a;
+        }
+        if (k < t.size()) s << ind << "  " << a << " = " << v << " ^ " << t[k] << ";\n";
+        else if (v != a) s << ind << "  " << a << " = " << v << ";\n";
+      } else {
+        s << ind << "  " << a << " = " << xor_chain(t) << ";\n";
+      }
+      live[i][b - b0] = true;
+    }
+  s << ind << "}\n";
+}
+
+// the inputs with a non-zero coefficient in some row
+std::vector<int> gfw_used(const uint32_t *mat, int R, int K) {
+  std::vector<int> used;
+  for (int j = 0; j < K; ++j)
+    for (int r = 0; r < R; ++r)
+      if (mat[r * K + j]) {
+        used.push_back(j);
+        break;
+      }
+  return used;
+}
+
+// Wave-pair split of the w = 32 network.  The one-wave form keeps R x 32
+// accumulator slices per lane (128 VGPRs at 4 rows) plus two inputs' 32 slices: 2 waves per SIMD.
+// Here the 4 waves of a block form 2 pairs; the two waves of a pair cover the same 64 lane
+// columns and each computes half of every output row's bit slices (role 0 slices 0-15, role 1
+// 16-31; balanced for any R).  Per step each wave loads and transposes one input (role 0 the even
+// used inputs, role 1 the odd), writes its 32 slices to LDS, XORs them into its half slices, and
+// after a barrier reads its partner's input slices from LDS into the same registers and XORs
+// those in: every input is still loaded and transposed once and the accumulators halve (64 VGPRs
+// at 4 rows).  At the end the halves meet through LDS: role 0 transposes and stores rows
+// 0 .. ceil(R/2)-1, role 1 the rest.  Tile: 128 lane columns x 16 B x 8 pieces, 2 KiB apart
+// (16 KiB per shard); LDS 2 pairs x 2 roles x 8 KiB.
+std::string gfw_rowsplit_source(const uint32_t *mat, int R, int K, int W) {
+  const int capv = (jit_variant() >> 8) & 255;
+  const int cap = capv == 0 ? 32 : capv == 255 ? 0 : capv;
+  const int tile = gfw_tile(W, R), HW = W / 2;
+  const int n0 = (R + 1) / 2;  // output rows of role 0: 0 .. n0-1; role 1: n0 .. R-1
+  std::vector<int> rows;
+  std::vector<std::string> acc;
+  for (int r = 0; r < R; ++r) {
+    rows.push_back(r);
+    acc.push_back("h" + std::to_string(r));
+  }
+  std::vector<std::vector<bool>> live0(R, std::vector<bool>(HW, false)), live1(R, std::vector<bool>(HW, false));
+  const std::vector<int> used = gfw_used(mat, R, K);
+  const int n = static_cast<int>(used.size()), steps = (n + 1) / 2;
+  std::ostringstream s;
+  gfw_prelude(s, R, K, W, 128 * 16);
+  s << "extern \"C\" __global__ __launch_bounds__(256) void lsec_xornet(Args a) {\n"
+       "  __shared__ u32x4 L[2][2][W / 4][64];\n"
+       "  const unsigned wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;\n"
+       "  const unsigned pair = wv >> 1, role = wv & 1;\n"
+       "  u32x4 (*const mine)[64] = L[pair][role];\n"
+       "  u32x4 (*const theirs)[64] = L[pair][role ^ 1];\n"
+       "  const long long C = a.size;\n"
+    << "  const unsigned tps = (unsigned)(C / " << tile << ");\n"
+    << "  const unsigned nt = tps * (unsigned)a.nstripes;\n"
+       "  const unsigned nb = gridDim.x, per = nb >> 3, rem = nb & 7, xcd = blockIdx.x & 7;\n"
+       "  const unsigned t0 = xcd * per + (xcd < rem ? xcd : rem) + (blockIdx.x >> 3);\n"
+       "  for (unsigned t = t0; t < nt; t += nb) {\n"
+       "    const unsigned s = t / tps;\n"
+    << "    const long long base = (long long)(t - s * tps) * " << tile << " + (pair * 64 + lane) * 16;\n";
+  for (int r = 0; r < R; ++r) s << "    u32 h" << r << "[" << HW << "];\n";
+  s << "    u32 e0[W], e1[W];\n";
+  auto ptr = [&](int j) {
+    return "a.in[" + std::to_string(j) + "].base + (unsigned long long)s * a.in[" + std::to_string(j) + "].stride + base";
+  };
+  // step u's own inputs into buffer b: used[2u] (role 0) and used[2u+1] (role 1)
+  auto load = [&](int u, int b) {
+    if (2 * u >= n) return;
+    if (2 * u + 1 < n)
+      s << "    ld(e" << b << ", role ? " << ptr(used[2 * u + 1]) << " : " << ptr(used[2 * u]) << ");\n";
+    else
+      s << "    if (role == 0) ld(e" << b << ", " << ptr(used[2 * u]) << ");\n";
+  };
+  // bit 20: no prefetch -- each step loads its own input at its top (32 fewer VGPRs live; the
+  // other waves of the SIMD hide the latency)
+  const bool ahead = !((jit_variant() >> 20) & 1);
+  if (ahead) load(0, 0);
+  for (int u = 0; u < steps; ++u) {
+    const int b = ahead ? u & 1 : 0;
+    const std::string e = "e" + std::to_string(b);
+    const bool pairB = 2 * u + 1 < n;
+    load(ahead ? u + 1 : u, ahead ? b ^ 1 : 0);
+    // own input: transpose, publish, accumulate.  A lone last input (odd count) is role 0's:
+    // role 1 then only reads it
+    if (pairB) {
+      s << "    tr(" << e << ");\n";
+    } else {
+      s << "    if (role == 0) tr(" << e << ");\n";
+    }
+    s << "    " << (pairB ? "" : "if (role == 0) ") << "{\n"
+      << "#pragma unroll\n      for (int q = 0; q < W / 4; ++q) mine[q][lane] = (u32x4){" << e << "[4 * q], " << e
+      << "[4 * q + 1], " << e << "[4 * q + 2], " << e << "[4 * q + 3]};\n    }\n";
+    if (pairB) {
+      s << "    if (role == 0) {\n";
+      gfw_net(s, mat, K, W, used[2 * u], rows, acc, live0, cap, e, "      ", 0, HW);
+      s << "    } else {\n";
+      gfw_net(s, mat, K, W, used[2 * u + 1], rows, acc, live1, cap, e, "      ", HW, W);
+      s << "    }\n";
+    } else {
+      s << "    if (role == 0) {\n";
+      gfw_net(s, mat, K, W, used[2 * u], rows, acc, live0, cap, e, "      ", 0, HW);
+      s << "    }\n";
+    }
+    s << "    __builtin_amdgcn_sched_barrier(0);\n    __syncthreads();\n";
+    // the partner's input from LDS, into the same registers
+    const std::string rd = "#pragma unroll\n      for (int q = 0; q < W / 4; ++q) { const u32x4 v = theirs[q][lane]; " + e + "[4 * q] = v.x; " + e +
+                           "[4 * q + 1] = v.y; " + e + "[4 * q + 2] = v.z; " + e + "[4 * q + 3] = v.w; }\n";
+    if (pairB) {
+      s << "    {\n" << rd << "    }\n    if (role == 0) {\n";
+      gfw_net(s, mat, K, W, used[2 * u + 1], rows, acc, live0, cap, e, "      ", 0, HW);
+      s << "    } else {\n";
+      gfw_net(s, mat, K, W, used[2 * u], rows, acc, live1, cap, e, "      ", HW, W);
+      s << "    }\n";
+    } else {
+      s << "    if (role == 1) {\n" << rd;
+      gfw_net(s, mat, K, W, used[2 * u], rows, acc, live1, cap, e, "      ", HW, W);
+      s << "    }\n";
+    }
+    s << "    __builtin_amdgcn_sched_barrier(0);\n    __syncthreads();\n";
+  }
+  // the halves meet: each role publishes its slices of the rows the other stores (slot k = the
+  // k-th of those rows, 4 quads each), then completes its own rows from the partner's slots
+  auto zero = [&](const std::vector<std::vector<bool>> &live) {
+    for (int r = 0; r < R; ++r)
+      for (int b = 0; b < HW; ++b)
+        if (!live[r][b]) s << "      h" << r << "[" << b << "] = 0u;\n";
+  };
+  auto publish = [&](int lo, int hi) {
+    for (int r = lo; r < hi; ++r)
+      for (int q = 0; q < HW / 4; ++q)
+        s << "      mine[" << (r - lo) * (HW / 4) + q << "][lane] = (u32x4){h" << r << "[" << 4 * q << "], h" << r << "["
+          << 4 * q + 1 << "], h" << r << "[" << 4 * q + 2 << "], h" << r << "[" << 4 * q + 3 << "]};\n";
+  };
+  auto complete = [&](int lo, int hi, bool low_half_mine) {
+    for (int r = lo; r < hi; ++r) {
+      s << "      { u32 f[W];\n";
+      for (int q = 0; q < HW / 4; ++q) {
+        const int mo = low_half_mine ? 4 * q : HW + 4 * q, po = low_half_mine ? HW + 4 * q : 4 * q;
+        s << "        { const u32x4 v = theirs[" << (r - lo) * (HW / 4) + q << "][lane]; f[" << po << "] = v.x; f[" << po + 1
+          << "] = v.y; f[" << po + 2 << "] = v.z; f[" << po + 3 << "] = v.w; }\n";
+        for (int d = 0; d < 4; ++d) s << "        f[" << mo + d << "] = h" << r << "[" << 4 * q + d << "];\n";
+      }
+      s << "        tr(f);\n        st(f, a.out[" << r << "].base + (unsigned long long)s * a.out[" << r << "].stride + base);\n      }\n";
+    }
+  };
+  s << "    if (role == 0) {\n";
+  zero(live0);
+  publish(n0, R);
+  s << "    } else {\n";
+  zero(live1);
+  publish(0, n0);
+  s << "    }\n    __syncthreads();\n    if (role == 0) {\n";
+  complete(0, n0, true);
+  s << "    } else {\n";
+  complete(n0, R, false);
+  s << "    }\n    __syncthreads();\n  }\n}\n";
+  return s.str();
+}
+
+// s_waitcnt immediate (gfx9 encoding) that waits for vmcnt <= n only
+int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
+
+// LDS-DMA ring form of the one-wave network (LSEC_JIT_VARIANT bit 22; bits 23-24: inputs in
+// flight D, 0 = 3).  At 4 rows x 32 slices the network holds one wave per SIMD, so the only cover
+// for HBM latency is how far ahead that wave's loads run; in registers that is one input (32
+// VGPRs each).  Here every input goes global -> LDS by global_load_lds_dwordx4 (no VGPR
+// destination) into a ring of D + 1 slots of 32 KiB (one slot per input: 8 pieces x 256 lanes x
+// 16 B, each wave's 1 KiB pieces contiguous as the DMA writes them), D inputs in flight.  The
+// grid is persistent (one block per CU, gfw_persistent) so the ring runs on across tiles: after
+// a tile's last input the next tile's first D inputs are issued, then the tile's stores.  A wave
+// reads back only what it loaded, so no barrier: the wave's own counted vmcnt retires an input
+// before its ds_reads, and an input refills the slot read one step earlier, whose reads have
+// completed.  The counts come from the issue order, the same in every tile (the body is one
+// basic block): the prologue issues R x 8 junk DMAs where the other tiles have the previous
+// tile's stores, and the last tile reloads its own first inputs where the others prefetch.
+std::string gfw_ring_source(const uint32_t *mat, int R, int K, int W) {
+  const int capv = (jit_variant() >> 8) & 255;
+  const int cap = capv == 0 ? 32 : capv == 255 ? 0 : capv;
+  const int tile = gfw_tile(W, R);
+  const std::vector<int> used = gfw_used(mat, R, K);
+  const int n = static_cast<int>(used.size());
+  const int dv = (jit_variant() >> 23) & 3;
+  const int D = std::max(1, std::min(n, dv == 0 ? 3 : dv)), S = D + 1;
+  const int P = W / 4;  // pieces (DMA instructions) per input per wave
+  std::ostringstream s;
+  gfw_prelude(s, R, K, W, 4096);
+  s << "#define LDSP(x) ((__attribute__((address_space(3))) void *)(x))\n"
+       "#define GLP(x) ((__attribute__((address_space(1))) void *)(x))\n"
        "extern \"C\" __global__ __launch_bounds__(256) void lsec_xornet(Args a) {\n"
+    << "  __shared__ u32x4 ring[" << S << "][W / 4][256];\n"
+    << "  const unsigned wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+       "  const long long C = a.size;\n"
+    << "  const unsigned tps = (unsigned)(C / " << tile << ");\n"
+    << "  const unsigned nt = tps * (unsigned)a.nstripes;\n"
+       "  const unsigned nb = gridDim.x, per = nb >> 3, rem = nb & 7, xcd = blockIdx.x & 7;\n"
+       "  const unsigned t0 = xcd * per + (xcd < rem ? xcd : rem) + (blockIdx.x >> 3);\n"
+       "  if (t0 >= nt) return;\n"
+       "  const unsigned lane16 = threadIdx.x * 16u;\n"
+       // the lane's LDS address of piece 0 of slot 0 (ds_read_b128 offsets add slot and piece)
+       "  const unsigned lds0 = (unsigned)(unsigned long long)LDSP(&ring[0][0][threadIdx.x]);\n"
+       // input j of tile tt, piece q: a wave-uniform base (2 SGPRs per input) plus a 32-bit
+       // lane offset (one VGPR per piece, shared by every input): the DMA's SGPR-base form
+       "#define UB(j, tt) ((const char *)(a.in[j].base + (unsigned long long)((tt) / tps) * a.in[j].stride + \\\n"
+    << "    (long long)((tt) - ((tt) / tps) * tps) * " << tile << "))\n"
+       "#define DMA(j, tt, sl) do { const char *ub_ = UB(j, tt); \\\n"
+       "    _Pragma(\"unroll\") for (int q_ = 0; q_ < W / 4; ++q_) \\\n"
+       "      __builtin_amdgcn_global_load_lds(GLP(ub_ + (lane16 + q_ * 4096u)), LDSP(&ring[sl][q_][wv * 64]), 16, 0, 2); } while (0)\n";
+  {
+    // the slot's ds_reads in asm: the compiler would order every read behind the youngest LDS
+    // DMA (vmcnt(0)); the counted vmcnt above each step orders them instead.  One statement for
+    // the reads and their lgkmcnt(0) wait, so no use of the results can be scheduled between
+    // them (the compiler does not track an asm's LDS results)
+    std::string ins, outs;
+    for (int q = 0; q < P; ++q) {
+      ins += "ds_read_b128 %" + std::to_string(q) + ", %" + std::to_string(P) + " offset:" + std::to_string(q * 4096) + "\\n\\t";
+      outs += std::string(q ? ", " : "") + "\"=&v\"(v_[" + std::to_string(q) + "])";
+    }
+    ins += "s_waitcnt lgkmcnt(0)";
+    s << "#define RD(e, sl) do { u32x4 v_[W / 4]; const unsigned a_ = lds0 + (sl) * (W / 4) * 4096u; \\\n"
+      << "    asm volatile(\"" << ins << "\" : " << outs << " : \"v\"(a_) : \"memory\"); \\\n"
+      << "    _Pragma(\"unroll\") for (int q_ = 0; q_ < W / 4; ++q_) { e[4 * q_] = v_[q_].x; e[4 * q_ + 1] = v_[q_].y; \\\n"
+         "      e[4 * q_ + 2] = v_[q_].z; e[4 * q_ + 3] = v_[q_].w; } } while (0)\n";
+  }
+  // issue order of one tile (the same for every tile after the first): the next tile's inputs
+  // 0 .. D-1 (issued after the previous tile's last step), the previous tile's R*P stores, then
+  // step u: wait, refill input u + D (< n), read, compute.  The first tile waits for its
+  // prologue DMAs outright, so its counts (fewer ops between) are met too
+  std::vector<int> ops;  // input index of this tile's DMAs, -1 other ops
+  for (int u = 0; u < D; ++u)
+    for (int q = 0; q < P; ++q) ops.push_back(u);
+  for (int q = 0; q < R * P; ++q) ops.push_back(-1);
+  std::vector<int> N(n);
+  for (int u = 0; u < n; ++u) {
+    size_t last = 0;
+    for (size_t i = 0; i < ops.size(); ++i)
+      if (ops[i] == u) last = i;
+    N[u] = static_cast<int>(ops.size() - 1 - last);
+    if (u + D < n)
+      for (int q = 0; q < P; ++q) ops.push_back(u + D);
+  }
+  s << "  unsigned slot = 0;\n";
+  for (int u = 0; u < D; ++u) s << "  DMA(" << used[u] << ", t0, " << u << ");\n";
+  s << "  __builtin_amdgcn_s_waitcnt(" << vmcnt_imm(0) << ");\n"
+       "  for (unsigned t = t0; t < nt; t += nb) {\n"
+       "    const unsigned tn = t + nb < nt ? t + nb : t;  // the last tile reloads its own inputs\n"
+       "    const unsigned s = t / tps;\n"
+    << "    const long long base = (long long)(t - s * tps) * " << tile << " + lane16;\n";
+  std::vector<std::string> acc;
+  std::vector<int> rows;
+  for (int r = 0; r < R; ++r) {
+    s << "    u32 h" << r << "[W];\n";
+    acc.push_back("h" + std::to_string(r));
+    rows.push_back(r);
+  }
+  s << "    u32 e[W];\n";
+  std::vector<std::vector<bool>> live(R, std::vector<bool>(W, false));
+  for (int u = 0; u < n; ++u) {
+    s << "    __builtin_amdgcn_s_waitcnt(" << vmcnt_imm(N[u]) << ");  // vmcnt(" << N[u] << "): input " << u << " landed\n"
+      << "    __builtin_amdgcn_sched_barrier(0);\n";
+    if (u + D < n) s << "    DMA(" << used[u + D] << ", t, (slot + " << D << ") % " << S << ");\n";
+    s << "    RD(e, slot);\n"
+      << "    slot = slot == " << S - 1 << " ? 0 : slot + 1;\n"
+      << "    tr(e);\n";
+    gfw_net(s, mat, K, W, used[u], rows, acc, live, cap, "e", "    ");
+    s << "    __builtin_amdgcn_sched_barrier(0);\n";
+  }
+  // the next tile's first inputs, into the slots the steps above continue with
+  for (int u = 0; u < D; ++u) s << "    DMA(" << used[u] << ", tn, (slot + " << u << ") % " << S << ");\n";
+  for (int r = 0; r < R; ++r) {
+    for (int b = 0; b < W; ++b)
+      if (!live[r][b]) s << "    h" << r << "[" << b << "] = 0u;\n";
+    s << "    tr(h" << r << ");\n    st(h" << r << ", a.out[" << r << "].base + (unsigned long long)s * a.out[" << r
+      << "].stride + base);\n";
+  }
+  s << "  }\n  __builtin_amdgcn_s_waitcnt(" << vmcnt_imm(0) << ");\n}\n";
+  return s.str();
+}
+
+}  // namespace
+
+std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
+  if (gfw_rowsplit(W, R)) return gfw_rowsplit_source(mat, R, K, W);
+  if (gfw_ring(W, R)) return gfw_ring_source(mat, R, K, W);
+  // LSEC_JIT_VARIANT bits 8-15: most shared pairs per input (0: the default 32, 255: none);
+  // bit 16: let the compiler schedule loads freely (no one-input-ahead prefetch fenced by sched
+  // barriers: it then hoists every input's loads and spills at 10+4, w = 32)
+  const int capv = (jit_variant() >> 8) & 255;
+  const int cap = capv == 0 ? 32 : capv == 255 ? 0 : capv;
+  const bool fenced = !((jit_variant() >> 16) & 1);
+  // bits 17-18: inputs loaded ahead of their use (0: the default 1)
+  const int ahead = std::max(1, (jit_variant() >> 17) & 3);
+  const int tile = gfw_tile(W, R);  // the launch covers whole tiles only
+  std::ostringstream s;
+  gfw_prelude(s, R, K, W, 4096);
+  s << "extern \"C\" __global__ __launch_bounds__(256) void lsec_xornet(Args a) {\n"
        "  const long long C = a.size;\n"
     << "  const unsigned tps = (unsigned)(C / " << tile << ");\n"
     << "  const unsigned nt = tps * (unsigned)a.nstripes;\n"
@@ -382,18 +728,18 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
        "  for (unsigned t = t0; t < nt; t += nb) {\n"
        "    const unsigned s = t / tps;\n"
     << "    const long long base = (long long)(t - s * tps) * " << tile << " + threadIdx.x * 16;\n";
-  for (int r = 0; r < R; ++r) s << "    u32 h" << r << "[W];\n";
+  std::vector<std::string> acc;
+  std::vector<int> rows;
+  for (int r = 0; r < R; ++r) {
+    s << "    u32 h" << r << "[W];\n";
+    acc.push_back("h" + std::to_string(r));
+    rows.push_back(r);
+  }
   std::vector<std::vector<bool>> live(R, std::vector<bool>(W, false));
   // inputs with a non-zero coefficient in some row, each loaded one input ahead of its use: the
   // scheduler would otherwise hoist every input's loads to the top (K x W registers live: spills
   // at 10+4, w = 32), so sched barriers fence each input's arithmetic
-  std::vector<int> used;
-  for (int j = 0; j < K; ++j)
-    for (int r = 0; r < R; ++r)
-      if (mat[r * K + j]) {
-        used.push_back(j);
-        break;
-      }
+  const std::vector<int> used = gfw_used(mat, R, K);
   const size_t nbuf = static_cast<size_t>(ahead) + 1;
   auto load = [&](size_t u) {
     const int j = used[u];
@@ -402,41 +748,10 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
   for (size_t b = 0; b < nbuf; ++b) s << "    u32 e" << b << "[W];\n";
   for (size_t u = 0; u < used.size() && u < static_cast<size_t>(ahead); ++u) load(u);
   for (size_t u = 0; u < used.size(); ++u) {
-    const int j = used[u];
     if (u + ahead < used.size()) load(u + ahead);
-    // the bitmatrix block of every row's coefficient c_rj: slice b of the output takes input
-    // slices x with bit b of c_rj * x^x set
-    std::vector<std::vector<int>> rows(static_cast<size_t>(R) * W);
-    bool any = false;
-    for (int r = 0; r < R; ++r) {
-      uint32_t cx = mat[r * K + j];
-      for (int x = 0; x < W && cx; ++x) {
-        for (int b = 0; b < W; ++b)
-          if ((cx >> b) & 1u) rows[static_cast<size_t>(r) * W + b].push_back(x);
-        cx = gfw_times_x(cx, W);
-      }
-      any |= mat[r * K + j] != 0;
-    }
-    (void)any;
-    std::vector<std::pair<int, int>> pairs;
-    if (cap > 0) share_slice_pairs(rows, W, cap, pairs);
-    s << "    { u32 (&e)[W] = e" << u % nbuf << ";\n      tr(e);\n";
-    for (size_t i = 0; i < pairs.size(); ++i) {
-      auto nm = [&](int x) { return x < W ? "e[" + std::to_string(x) + "]" : "p" + std::to_string(x - W); };
-      s << "      const u32 p" << i << " = " << nm(pairs[i].first) << " ^ " << nm(pairs[i].second) << ";\n";
-    }
-    for (int r = 0; r < R; ++r)
-      for (int b = 0; b < W; ++b) {
-        const auto &row = rows[static_cast<size_t>(r) * W + b];
-        if (row.empty()) continue;
-        std::vector<std::string> t;
-        const std::string acc = "h" + std::to_string(r) + "[" + std::to_string(b) + "]";
-        if (live[r][b]) t.push_back(acc);
-        for (int x : row) t.push_back(x < W ? "e[" + std::to_string(x) + "]" : "p" + std::to_string(x - W));
-        s << "      " << acc << " = " << xor_chain(t) << ";\n";
-        live[r][b] = true;
-      }
-    s << "    }\n";
+    const std::string e = "e" + std::to_string(u % nbuf);
+    s << "    tr(" << e << ");\n";
+    gfw_net(s, mat, K, W, used[u], rows, acc, live, cap, e, "    ");
     if (fenced) s << "    __builtin_amdgcn_sched_barrier(0);\n";
   }
   for (int r = 0; r < R; ++r) {
@@ -493,6 +808,7 @@ std::vector<uint32_t> key_of(const uint32_t *mat, int R, int K, int w) {
 }
 
 void compile(std::shared_ptr<Entry> e) {
+  const auto t0 = std::chrono::steady_clock::now();
   std::string src;
   if (e->w == 8) {
     std::vector<uint8_t> m8(e->mat.begin(), e->mat.end());
@@ -523,7 +839,8 @@ void compile(std::shared_ptr<Entry> e) {
   }
   static const bool trace = getenv("LSEC_TRACE") != nullptr;
   if (trace || !err.empty())
-    fprintf(stderr, "[lsec jit] %dx%d w=%d xor network: %s\n", e->R, e->K, e->w, err.empty() ? "compiled" : err.c_str());
+    fprintf(stderr, "[lsec jit] %dx%d w=%d xor network: %s (%.2f s)\n", e->R, e->K, e->w, err.empty() ? "compiled" : err.c_str(),
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
   std::lock_guard<std::mutex> lk(g_mu);
   e->code.swap(code);
   e->err = err;
@@ -645,11 +962,21 @@ hipError_t launch(hipFunction_t fn, int R, int K, const ShardRef *in, const Shar
   std::memcpy(args.data() + 16 + sizeof(ShardRef) * K, out, sizeof(ShardRef) * R);
   size_t bytes = args.size();
   void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes, HIP_LAUNCH_PARAM_END};
-  const int64_t tile = w == 8 ? xornet_tile(K) : gfw_tile(w);  // as xornet_source / gfw_source
+  const int64_t tile = w == 8 ? xornet_tile(K) : gfw_tile(w, R);  // as xornet_source / gfw_source
   const uint64_t ntiles = static_cast<uint64_t>((size + tile - 1) / tile) * static_cast<uint64_t>(nstripes);
   if (ntiles == 0) return hipSuccess;
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
-  return hipModuleLaunchKernel(fn, static_cast<unsigned>(ntiles), 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+  uint64_t grid = ntiles;
+  if (w != 8 && gfw_ring(w, R)) {  // persistent: one block per CU, the ring runs on across tiles
+    static const int cus = [] {
+      int d = 0, n = 0;
+      if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+        n = 256;
+      return std::max(8, n);
+    }();
+    grid = std::min<uint64_t>(ntiles, static_cast<uint64_t>(cus));
+  }
+  return hipModuleLaunchKernel(fn, static_cast<unsigned>(grid), 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
 }
 
 }  // namespace jit

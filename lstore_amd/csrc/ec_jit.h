@@ -23,8 +23,13 @@ bool wants_gfw_net(int R, int K, int w);
 std::string xornet_source(const uint8_t *mat, int R, int K);
 // HIP source of the bit-sliced network for an R x K GF(2^w) matrix, w = 16 / 32
 std::string gfw_source(const uint32_t *mat, int R, int K, int w);
-// bytes of a shard one block of a w = 16 / 32 network covers per tile; it serves whole tiles only
-int gfw_tile(int w);
+// bytes of a shard one block of an R-row w = 16 / 32 network covers per tile; it serves whole
+// tiles only
+int gfw_tile(int w, int R);
+// whether the R-row network at w takes the wave-pair row split (ec_jit.cpp)
+bool gfw_rowsplit(int w, int R);
+// whether it takes the LDS-DMA ring form (persistent grid: one block per CU; ec_jit.cpp)
+bool gfw_ring(int w, int R);
 // bytes of a shard one 256-lane block of the network covers per tile
 int xornet_tile(int K);
 // LSEC_JIT_VARIANT (code shape knobs for A/B runs; 0 = default)
@@ -41,7 +46,7 @@ int wait(const void *image, int timeout_ms);
 // The compiled network for `image` on the current device, or nullptr (not bound / not ready).
 hipFunction_t ready(const void *image, int R, int K);
 // out[r] = sum_j A[r][j] in[j] for every stripe (same shard addressing as ApplyArgs); at
-// w = 16 / 32 over the first size / gfw_tile(w) whole tiles of every shard only.
+// w = 16 / 32 over the first size / gfw_tile(w, R) whole tiles of every shard only.
 hipError_t launch(hipFunction_t fn, int R, int K, const ShardRef *in, const ShardRef *out, int nstripes, int64_t size,
                   hipStream_t st, int w = 8);
 

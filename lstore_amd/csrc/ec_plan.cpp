@@ -564,7 +564,7 @@ int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in,
   if (net) {
     if (hipFunction_t fn = lsec::jit::ready(image, R, K)) {  // the matrix's compiled XOR network
       // w = 16 / 32 networks take whole tiles only: the tail columns go to the generic kernel
-      const long long whole = kind == KWORDWISE ? size / lsec::jit::gfw_tile(w) * lsec::jit::gfw_tile(w) : size;
+      const long long whole = kind == KWORDWISE ? size / lsec::jit::gfw_tile(w, R) * lsec::jit::gfw_tile(w, R) : size;
       // batches split so tile indices stay 32-bit, as below
       const long long per = std::max(1LL, (1LL << 30) / std::max(1LL, size / 4096 + 1));
       ShardRef bi[lsec::jit::kMaxCols], bo[lsec::jit::kMaxRows];

@@ -440,6 +440,8 @@ def test_xor_network_vs_oracle(cuda, k, m, size):
     (L.REED_SOL_VAN, 20, 6, 16, 16384 + 8, [0, 5, 7, 11, 13, 19]),
     (L.REED_SOL_R6_OP, 6, 2, 32, 32768 + 24, [0, 4]),
     (L.REED_SOL_VAN, 4, 2, 32, 8, [0, 1]),                  # smaller than one tile: generic kernel only
+    (L.REED_SOL_VAN, 5, 3, 32, 5 * 16384 + 16, [0, 2, 4]),  # odd input count: a lone last input per tile
+    (L.REED_SOL_VAN, 7, 4, 32, 3 * 16384, [1, 7, 8, 10]),   # decode mixing data and coding losses
 ])
 def test_gfw_network_vs_oracle(cuda, method, k, m, w, size, lost):
     """RS / r6 at w = 16 / 32 run on their compiled bit-sliced XOR networks (ec_jit.cpp,

@@ -61,6 +61,11 @@ def main():
         out = torch.empty((N, 1, C), dtype=torch.uint8, device=dev)
         plan.prepare_encode()  # wide codes: wait for the compiled XOR network (variant 0,0 uses it)
         plan.prepare_decode([0])
+        import time
+        t_end = time.time() + 240  # heavy networks can take longer than prepare's 30 s wait
+        while time.time() < t_end and not plan.jit():  # (a lost-D0 decode may be XOR-only: no network)
+            time.sleep(1)
+        print(f"{name}: encode network {'ready' if plan.jit() else 'NOT ready'}", flush=True)
         plan.encode_dev(data, par)
         ref_par = par.clone()
         stream = torch.cuda.current_stream()
