@@ -96,7 +96,10 @@ bool wants_xornet(int R, int K) {
 // bit 1 = doubling by shift-and-subtract instead of a packed 16-bit multiply, bits 4-7 = dwords
 // per lane (1, 2, 4; 0 = 4).  Measured on RS(20+6) (profiles/r02_v15_jit_ab.txt): all shapes
 // within 70.6-74.3 % of 8 TB/s, the default (4 dwords, packed multiply, no pair elimination)
-// best; pair elimination cuts VALU instructions 20 % but not time.
+// best; pair elimination cuts VALU instructions 20 % but not time.  w = 16 / 32 networks: bits
+// 8-15 shared-pair cap, 16 unfenced loads, 17-18 inputs ahead (gfw_source); 19 the wave-pair
+// slice split at w = 32, 20 its no-prefetch form, 21 serial XOR folds -- all slower than the
+// default on RS(10+4) w = 32 (profiles/r04_v7_gfw_w32_ab.md).
 int jit_variant() {
   static const int v = [] {
     const char *s = getenv("LSEC_JIT_VARIANT");
@@ -322,11 +325,6 @@ void share_slice_pairs(std::vector<std::vector<int>> &rows, int W, int cap, std:
 bool gfw_rowsplit(int w, int R) {
   // LSEC_JIT_VARIANT bit 19: the wave-pair row split below (w = 32, 3-4 rows)
   return w == 32 && R >= 3 && ((jit_variant() >> 19) & 1);
-}
-
-bool gfw_ring(int w, int R) {
-  // LSEC_JIT_VARIANT bit 22: the LDS-DMA ring below (not with the row split)
-  return (w == 16 || w == 32) && !gfw_rowsplit(w, R) && ((jit_variant() >> 22) & 1);
 }
 
 int gfw_tile(int w, int R) { return gfw_rowsplit(w, R) ? 128 * 4 * w : 256 * 4 * w; }
@@ -584,130 +582,10 @@ std::string gfw_rowsplit_source(const uint32_t *mat, int R, int K, int W) {
   return s.str();
 }
 
-// s_waitcnt immediate (gfx9 encoding) that waits for vmcnt <= n only
-int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
-
-// LDS-DMA ring form of the one-wave network (LSEC_JIT_VARIANT bit 22; bits 23-24: inputs in
-// flight D, 0 = 3).  At 4 rows x 32 slices the network holds one wave per SIMD, so the only cover
-// for HBM latency is how far ahead that wave's loads run; in registers that is one input (32
-// VGPRs each).  Here every input goes global -> LDS by global_load_lds_dwordx4 (no VGPR
-// destination) into a ring of D + 1 slots of 32 KiB (one slot per input: 8 pieces x 256 lanes x
-// 16 B, each wave's 1 KiB pieces contiguous as the DMA writes them), D inputs in flight.  The
-// grid is persistent (one block per CU, gfw_persistent) so the ring runs on across tiles: after
-// a tile's last input the next tile's first D inputs are issued, then the tile's stores.  A wave
-// reads back only what it loaded, so no barrier: the wave's own counted vmcnt retires an input
-// before its ds_reads, and an input refills the slot read one step earlier, whose reads have
-// completed.  The counts come from the issue order, the same in every tile (the body is one
-// basic block): the prologue issues R x 8 junk DMAs where the other tiles have the previous
-// tile's stores, and the last tile reloads its own first inputs where the others prefetch.
-std::string gfw_ring_source(const uint32_t *mat, int R, int K, int W) {
-  const int capv = (jit_variant() >> 8) & 255;
-  const int cap = capv == 0 ? 32 : capv == 255 ? 0 : capv;
-  const int tile = gfw_tile(W, R);
-  const std::vector<int> used = gfw_used(mat, R, K);
-  const int n = static_cast<int>(used.size());
-  const int dv = (jit_variant() >> 23) & 3;
-  const int D = std::max(1, std::min(n, dv == 0 ? 3 : dv)), S = D + 1;
-  const int P = W / 4;  // pieces (DMA instructions) per input per wave
-  std::ostringstream s;
-  gfw_prelude(s, R, K, W, 4096);
-  s << "#define LDSP(x) ((__attribute__((address_space(3))) void *)(x))\n"
-       "#define GLP(x) ((__attribute__((address_space(1))) void *)(x))\n"
-       "extern \"C\" __global__ __launch_bounds__(256) void lsec_xornet(Args a) {\n"
-    << "  __shared__ u32x4 ring[" << S << "][W / 4][256];\n"
-    << "  const unsigned wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
-       "  const long long C = a.size;\n"
-    << "  const unsigned tps = (unsigned)(C / " << tile << ");\n"
-    << "  const unsigned nt = tps * (unsigned)a.nstripes;\n"
-       "  const unsigned nb = gridDim.x, per = nb >> 3, rem = nb & 7, xcd = blockIdx.x & 7;\n"
-       "  const unsigned t0 = xcd * per + (xcd < rem ? xcd : rem) + (blockIdx.x >> 3);\n"
-       "  if (t0 >= nt) return;\n"
-       "  const unsigned lane16 = threadIdx.x * 16u;\n"
-       // the lane's LDS address of piece 0 of slot 0 (ds_read_b128 offsets add slot and piece)
-       "  const unsigned lds0 = (unsigned)(unsigned long long)LDSP(&ring[0][0][threadIdx.x]);\n"
-       // input j of tile tt, piece q: a wave-uniform base (2 SGPRs per input) plus a 32-bit
-       // lane offset (one VGPR per piece, shared by every input): the DMA's SGPR-base form
-       "#define UB(j, tt) ((const char *)(a.in[j].base + (unsigned long long)((tt) / tps) * a.in[j].stride + \\\n"
-    << "    (long long)((tt) - ((tt) / tps) * tps) * " << tile << "))\n"
-       "#define DMA(j, tt, sl) do { const char *ub_ = UB(j, tt); \\\n"
-       "    _Pragma(\"unroll\") for (int q_ = 0; q_ < W / 4; ++q_) \\\n"
-       "      __builtin_amdgcn_global_load_lds(GLP(ub_ + (lane16 + q_ * 4096u)), LDSP(&ring[sl][q_][wv * 64]), 16, 0, 2); } while (0)\n";
-  {
-    // the slot's ds_reads in asm: the compiler would order every read behind the youngest LDS
-    // DMA (vmcnt(0)); the counted vmcnt above each step orders them instead.  One statement for
-    // the reads and their lgkmcnt(0) wait, so no use of the results can be scheduled between
-    // them (the compiler does not track an asm's LDS results)
-    std::string ins, outs;
-    for (int q = 0; q < P; ++q) {
-      ins += "ds_read_b128 %" + std::to_string(q) + ", %" + std::to_string(P) + " offset:" + std::to_string(q * 4096) + "\\n\\t";
-      outs += std::string(q ? ", " : "") + "\"=&v\"(v_[" + std::to_string(q) + "])";
-    }
-    ins += "s_waitcnt lgkmcnt(0)";
-    s << "#define RD(e, sl) do { u32x4 v_[W / 4]; const unsigned a_ = lds0 + (sl) * (W / 4) * 4096u; \\\n"
-      << "    asm volatile(\"" << ins << "\" : " << outs << " : \"v\"(a_) : \"memory\"); \\\n"
-      << "    _Pragma(\"unroll\") for (int q_ = 0; q_ < W / 4; ++q_) { e[4 * q_] = v_[q_].x; e[4 * q_ + 1] = v_[q_].y; \\\n"
-         "      e[4 * q_ + 2] = v_[q_].z; e[4 * q_ + 3] = v_[q_].w; } } while (0)\n";
-  }
-  // issue order of one tile (the same for every tile after the first): the next tile's inputs
-  // 0 .. D-1 (issued after the previous tile's last step), the previous tile's R*P stores, then
-  // step u: wait, refill input u + D (< n), read, compute.  The first tile waits for its
-  // prologue DMAs outright, so its counts (fewer ops between) are met too
-  std::vector<int> ops;  // input index of this tile's DMAs, -1 other ops
-  for (int u = 0; u < D; ++u)
-    for (int q = 0; q < P; ++q) ops.push_back(u);
-  for (int q = 0; q < R * P; ++q) ops.push_back(-1);
-  std::vector<int> N(n);
-  for (int u = 0; u < n; ++u) {
-    size_t last = 0;
-    for (size_t i = 0; i < ops.size(); ++i)
-      if (ops[i] == u) last = i;
-    N[u] = static_cast<int>(ops.size() - 1 - last);
-    if (u + D < n)
-      for (int q = 0; q < P; ++q) ops.push_back(u + D);
-  }
-  s << "  unsigned slot = 0;\n";
-  for (int u = 0; u < D; ++u) s << "  DMA(" << used[u] << ", t0, " << u << ");\n";
-  s << "  __builtin_amdgcn_s_waitcnt(" << vmcnt_imm(0) << ");\n"
-       "  for (unsigned t = t0; t < nt; t += nb) {\n"
-       "    const unsigned tn = t + nb < nt ? t + nb : t;  // the last tile reloads its own inputs\n"
-       "    const unsigned s = t / tps;\n"
-    << "    const long long base = (long long)(t - s * tps) * " << tile << " + lane16;\n";
-  std::vector<std::string> acc;
-  std::vector<int> rows;
-  for (int r = 0; r < R; ++r) {
-    s << "    u32 h" << r << "[W];\n";
-    acc.push_back("h" + std::to_string(r));
-    rows.push_back(r);
-  }
-  s << "    u32 e[W];\n";
-  std::vector<std::vector<bool>> live(R, std::vector<bool>(W, false));
-  for (int u = 0; u < n; ++u) {
-    s << "    __builtin_amdgcn_s_waitcnt(" << vmcnt_imm(N[u]) << ");  // vmcnt(" << N[u] << "): input " << u << " landed\n"
-      << "    __builtin_amdgcn_sched_barrier(0);\n";
-    if (u + D < n) s << "    DMA(" << used[u + D] << ", t, (slot + " << D << ") % " << S << ");\n";
-    s << "    RD(e, slot);\n"
-      << "    slot = slot == " << S - 1 << " ? 0 : slot + 1;\n"
-      << "    tr(e);\n";
-    gfw_net(s, mat, K, W, used[u], rows, acc, live, cap, "e", "    ");
-    s << "    __builtin_amdgcn_sched_barrier(0);\n";
-  }
-  // the next tile's first inputs, into the slots the steps above continue with
-  for (int u = 0; u < D; ++u) s << "    DMA(" << used[u] << ", tn, (slot + " << u << ") % " << S << ");\n";
-  for (int r = 0; r < R; ++r) {
-    for (int b = 0; b < W; ++b)
-      if (!live[r][b]) s << "    h" << r << "[" << b << "] = 0u;\n";
-    s << "    tr(h" << r << ");\n    st(h" << r << ", a.out[" << r << "].base + (unsigned long long)s * a.out[" << r
-      << "].stride + base);\n";
-  }
-  s << "  }\n  __builtin_amdgcn_s_waitcnt(" << vmcnt_imm(0) << ");\n}\n";
-  return s.str();
-}
-
 }  // namespace
 
 std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
   if (gfw_rowsplit(W, R)) return gfw_rowsplit_source(mat, R, K, W);
-  if (gfw_ring(W, R)) return gfw_ring_source(mat, R, K, W);
   // LSEC_JIT_VARIANT bits 8-15: most shared pairs per input (0: the default 32, 255: none);
   // bit 16: let the compiler schedule loads freely (no one-input-ahead prefetch fenced by sched
   // barriers: it then hoists every input's loads and spills at 10+4, w = 32)
@@ -966,17 +844,7 @@ hipError_t launch(hipFunction_t fn, int R, int K, const ShardRef *in, const Shar
   const uint64_t ntiles = static_cast<uint64_t>((size + tile - 1) / tile) * static_cast<uint64_t>(nstripes);
   if (ntiles == 0) return hipSuccess;
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
-  uint64_t grid = ntiles;
-  if (w != 8 && gfw_ring(w, R)) {  // persistent: one block per CU, the ring runs on across tiles
-    static const int cus = [] {
-      int d = 0, n = 0;
-      if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-        n = 256;
-      return std::max(8, n);
-    }();
-    grid = std::min<uint64_t>(ntiles, static_cast<uint64_t>(cus));
-  }
-  return hipModuleLaunchKernel(fn, static_cast<unsigned>(grid), 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+  return hipModuleLaunchKernel(fn, static_cast<unsigned>(ntiles), 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
 }
 
 }  // namespace jit

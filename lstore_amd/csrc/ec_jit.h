@@ -28,8 +28,6 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int w);
 int gfw_tile(int w, int R);
 // whether the R-row network at w takes the wave-pair row split (ec_jit.cpp)
 bool gfw_rowsplit(int w, int R);
-// whether it takes the LDS-DMA ring form (persistent grid: one block per CU; ec_jit.cpp)
-bool gfw_ring(int w, int R);
 // bytes of a shard one 256-lane block of the network covers per tile
 int xornet_tile(int K);
 // LSEC_JIT_VARIANT (code shape knobs for A/B runs; 0 = default)
