@@ -51,14 +51,11 @@ bool is_pinned_host(const void *ptr) {
   return i.ok && i.type == hipMemoryTypeHost;
 }
 
-// every staged shard of the first and last stripe pinned?  (a stray pageable pointer in
-// between stays correct -- hipMemcpyAsync accepts pageable memory too, only slower)
 // Ranges pinned in place by a running call (InPlacePin), page-rounded.  Another call that
 // touches them must not take them for caller-pinned memory: the owner unregisters them when
 // it returns, maybe while the other call's DMA is still queued.
 std::mutex g_inplace_mu;
 std::vector<std::pair<uintptr_t, uintptr_t>> g_inplace;
-
 
 bool inplace_overlaps_locked(uintptr_t lo, uintptr_t hi) {
   for (const auto &r : g_inplace)
@@ -118,16 +115,17 @@ bool caller_pinned_aliases(char **ptrs, int nstripes, int km, const std::vector<
 CallerPinned caller_pinned(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
                            long long C, bool kernel_ok) {
   CallerPinned r;
+  if (nstripes < 1) return r;
   // A first chunk that is not page-locked settles it, with no lock: every path below returns
   // "not pinned" for it too, and taking memory for pageable is always safe.  (Per-stripe calls
   // from hundreds of threads queued on this mutex.)
-  if (nstripes >= 1 && tl_memo_depth > 0)
+  if (tl_memo_depth > 0)
     for (const auto &kv : tl_memo)  // a chunk of this call already known not to be page-locked
       if (!kv.second.ok || kv.second.type != hipMemoryTypeHost)
         for (const std::vector<int> *ids : {&in_ids, &out_ids})
           for (int id : *ids)
             if (ptrs[id] == kv.first) return r;
-  if (!in_ids.empty() && nstripes >= 1 && !is_pinned_host(ptrs[in_ids[0]])) return r;
+  if (!in_ids.empty() && !is_pinned_host(ptrs[in_ids[0]])) return r;
   std::lock_guard<std::mutex> lk(g_inplace_mu);
   if (!g_inplace.empty()) {
     for (int s = 0; s < nstripes; ++s)
@@ -137,6 +135,9 @@ CallerPinned caller_pinned(char **ptrs, int nstripes, int km, const std::vector<
           if (inplace_overlaps_locked(a & ~(kPage - 1), (a + static_cast<uintptr_t>(C) + kPage - 1) & ~(kPage - 1))) return r;
         }
   }
+  // every staged shard of the first and last stripe page-locked?  (a stray pageable pointer in
+  // between stays correct for DMA -- hipMemcpyAsync accepts pageable memory too, only slower;
+  // the kernel transport checks every chunk, caller_pinned_aliases)
   std::vector<PinnedAlloc> seen;
   uint64_t d = 0;
   for (int s : {0, nstripes - 1}) {
