@@ -97,9 +97,9 @@ bool wants_xornet(int R, int K) {
 // per lane (1, 2, 4; 0 = 4).  Measured on RS(20+6) (profiles/r02_v15_jit_ab.txt): all shapes
 // within 70.6-74.3 % of 8 TB/s, the default (4 dwords, packed multiply, no pair elimination)
 // best; pair elimination cuts VALU instructions 20 % but not time.  w = 16 / 32 networks: bits
-// 8-15 shared-pair cap, 16 unfenced loads, 17-18 inputs ahead (gfw_source); 19 the wave-pair
-// slice split at w = 32, 20 its no-prefetch form, 21 serial XOR folds -- all slower than the
-// default on RS(10+4) w = 32 (profiles/r04_v7_gfw_w32_ab.md).
+// 8-15 shared-pair cap, 16 unfenced loads, 17-18 inputs ahead, 21 serial XOR folds (gfw_source);
+// 19 turns the wave-pair split of 4-row w = 32 networks off, 20-23 shape it
+// (gfw_rowsplit_source; profiles/r04_v7_gfw_w32_ab.md, r04_v9_gfw_w32_split.txt).
 int jit_variant() {
   static const int v = [] {
     const char *s = getenv("LSEC_JIT_VARIANT");
@@ -323,8 +323,10 @@ void share_slice_pairs(std::vector<std::vector<int>> &rows, int W, int cap, std:
 }  // namespace
 
 bool gfw_rowsplit(int w, int R) {
-  // LSEC_JIT_VARIANT bit 19: the wave-pair row split below (w = 32, 3-4 rows)
-  return w == 32 && R >= 3 && ((jit_variant() >> 19) & 1);
+  // the wave-pair split below for 4-row networks at w = 32, where the one-wave form holds one
+  // wave per SIMD (RS(10+4) encode 0.66 -> 0.76; at 3 rows the one-wave form holds two and the
+  // split gains nothing: profiles/r04_v9_gfw_w32_split.txt).  LSEC_JIT_VARIANT bit 19 turns it off
+  return w == 32 && R >= 4 && !((jit_variant() >> 19) & 1);
 }
 
 int gfw_tile(int w, int R) { return gfw_rowsplit(w, R) ? 128 * 4 * w : 256 * 4 * w; }
@@ -380,8 +382,9 @@ void gfw_prelude(std::ostringstream &s, int R, int K, int W, int stride) {
 // bitmatrix block of the coefficient -- after common-pair elimination over those rows
 void gfw_net(std::ostringstream &s, const uint32_t *mat, int K, int W, int j, const std::vector<int> &rows,
              const std::vector<std::string> &acc, std::vector<std::vector<bool>> &live, int cap, const std::string &e,
-             const char *ind, int b0 = 0, int b1 = -1) {
-  // output slices b0 .. b1-1 only (accumulator element b - b0)
+             const char *ind, bool linear, int b0 = 0, int b1 = -1) {
+  // output slices b0 .. b1-1 only (accumulator element b - b0); linear: serial folds into the
+  // accumulator instead of balanced 3-input XOR trees
   if (b1 < 0) b1 = W;
   std::vector<std::vector<int>> sl(rows.size() * W);
   bool any = false;
@@ -397,8 +400,6 @@ void gfw_net(std::ostringstream &s, const uint32_t *mat, int K, int W, int j, co
   if (!any) return;
   std::vector<std::pair<int, int>> pairs;
   if (cap > 0) share_slice_pairs(sl, W, cap, pairs);
-  // LSEC_JIT_VARIANT bit 21: serial folds (below) instead of balanced 3-input XOR trees
-  const bool linear = (jit_variant() >> 21) & 1;
   auto nm = [&](int x) { return x < W ? e + "[" + std::to_string(x) + "]" : "p" + std::to_string(x - W); };
   s << ind << "{\n";
   for (size_t i = 0; i < pairs.size(); ++i)
@@ -443,8 +444,8 @@ std::vector<int> gfw_used(const uint32_t *mat, int R, int K) {
 }
 
 // Wave-pair split of the w = 32 network.  The one-wave form keeps R x 32
-// accumulator slices per lane (128 VGPRs at 4 rows) plus two inputs' 32 slices: 2 waves per SIMD.
-// Here the 4 waves of a block form 2 pairs; the two waves of a pair cover the same 64 lane
+// accumulator slices per lane (128 VGPRs at 4 rows) plus two inputs' 32 slices: at 4 rows its code
+// object takes 273 registers, one wave per SIMD.  Here the 4 waves of a block form 2 pairs; the two waves of a pair cover the same 64 lane
 // columns and each computes half of every output row's bit slices (role 0 slices 0-15, role 1
 // 16-31; balanced for any R).  Per step each wave loads and transposes one input (role 0 the even
 // used inputs, role 1 the odd), writes its 32 slices to LDS, XORs them into its half slices, and
@@ -452,7 +453,10 @@ std::vector<int> gfw_used(const uint32_t *mat, int R, int K) {
 // those in: every input is still loaded and transposed once and the accumulators halve (64 VGPRs
 // at 4 rows).  At the end the halves meet through LDS: role 0 transposes and stores rows
 // 0 .. ceil(R/2)-1, role 1 the rest.  Tile: 128 lane columns x 16 B x 8 pieces, 2 KiB apart
-// (16 KiB per shard); LDS 2 pairs x 2 roles x 8 KiB.
+// (16 KiB per shard); LDS 2 pairs x 2 roles x 8 KiB.  The roles' code sits in two consecutive
+// `if (role == r)` blocks, never in if / else: at an if / else join the compiler kept both
+// branches' accumulators apart (294 registers at RS(10+4) even with identical branches; 139 as
+// consecutive ifs, profiles/r04_v7_gfw_w32_ab.md).
 std::string gfw_rowsplit_source(const uint32_t *mat, int R, int K, int W) {
   const int capv = (jit_variant() >> 8) & 255;
   const int cap = capv == 0 ? 32 : capv == 255 ? 0 : capv;
@@ -468,8 +472,16 @@ std::string gfw_rowsplit_source(const uint32_t *mat, int R, int K, int W) {
   const std::vector<int> used = gfw_used(mat, R, K);
   const int n = static_cast<int>(used.size()), steps = (n + 1) / 2;
   std::ostringstream s;
+  // defaults measured best (profiles/r04_v9_gfw_w32_split.txt): serial folds (LSEC_JIT_VARIANT
+  // bit 21: trees instead), one input prefetched (bit 20: none), and an occupancy target of 3
+  // waves per SIMD for the register allocator (bits 22-23: 1 none, 2 four, 3 two), which RS(10+4)
+  // meets at 167 registers without spills
+  const bool linear = !((jit_variant() >> 21) & 1);
+  const int wv_opt = (jit_variant() >> 22) & 3, wpe = wv_opt == 0 ? 3 : wv_opt == 1 ? 0 : wv_opt == 2 ? 4 : 2;
   gfw_prelude(s, R, K, W, 128 * 16);
-  s << "extern \"C\" __global__ __launch_bounds__(256) void lsec_xornet(Args a) {\n"
+  s << "extern \"C\" __global__ __launch_bounds__(256) ";
+  if (wpe) s << "__attribute__((amdgpu_waves_per_eu(" << wpe << "))) ";
+  s << "void lsec_xornet(Args a) {\n"
        "  __shared__ u32x4 L[2][2][W / 4][64];\n"
        "  const unsigned wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;\n"
        "  const unsigned pair = wv >> 1, role = wv & 1;\n"
@@ -517,13 +529,13 @@ std::string gfw_rowsplit_source(const uint32_t *mat, int R, int K, int W) {
       << "[4 * q + 1], " << e << "[4 * q + 2], " << e << "[4 * q + 3]};\n    }\n";
     if (pairB) {
       s << "    if (role == 0) {\n";
-      gfw_net(s, mat, K, W, used[2 * u], rows, acc, live0, cap, e, "      ", 0, HW);
-      s << "    } else {\n";
-      gfw_net(s, mat, K, W, used[2 * u + 1], rows, acc, live1, cap, e, "      ", HW, W);
+      gfw_net(s, mat, K, W, used[2 * u], rows, acc, live0, cap, e, "      ", linear, 0, HW);
+      s << "    }\n    if (role == 1) {\n";
+      gfw_net(s, mat, K, W, used[2 * u + 1], rows, acc, live1, cap, e, "      ", linear, HW, W);
       s << "    }\n";
     } else {
       s << "    if (role == 0) {\n";
-      gfw_net(s, mat, K, W, used[2 * u], rows, acc, live0, cap, e, "      ", 0, HW);
+      gfw_net(s, mat, K, W, used[2 * u], rows, acc, live0, cap, e, "      ", linear, 0, HW);
       s << "    }\n";
     }
     s << "    __builtin_amdgcn_sched_barrier(0);\n    __syncthreads();\n";
@@ -532,13 +544,13 @@ std::string gfw_rowsplit_source(const uint32_t *mat, int R, int K, int W) {
                            "[4 * q + 1] = v.y; " + e + "[4 * q + 2] = v.z; " + e + "[4 * q + 3] = v.w; }\n";
     if (pairB) {
       s << "    {\n" << rd << "    }\n    if (role == 0) {\n";
-      gfw_net(s, mat, K, W, used[2 * u + 1], rows, acc, live0, cap, e, "      ", 0, HW);
-      s << "    } else {\n";
-      gfw_net(s, mat, K, W, used[2 * u], rows, acc, live1, cap, e, "      ", HW, W);
+      gfw_net(s, mat, K, W, used[2 * u + 1], rows, acc, live0, cap, e, "      ", linear, 0, HW);
+      s << "    }\n    if (role == 1) {\n";
+      gfw_net(s, mat, K, W, used[2 * u], rows, acc, live1, cap, e, "      ", linear, HW, W);
       s << "    }\n";
     } else {
       s << "    if (role == 1) {\n" << rd;
-      gfw_net(s, mat, K, W, used[2 * u], rows, acc, live1, cap, e, "      ", HW, W);
+      gfw_net(s, mat, K, W, used[2 * u], rows, acc, live1, cap, e, "      ", linear, HW, W);
       s << "    }\n";
     }
     s << "    __builtin_amdgcn_sched_barrier(0);\n    __syncthreads();\n";
@@ -571,12 +583,12 @@ std::string gfw_rowsplit_source(const uint32_t *mat, int R, int K, int W) {
   s << "    if (role == 0) {\n";
   zero(live0);
   publish(n0, R);
-  s << "    } else {\n";
+  s << "    }\n    if (role == 1) {\n";
   zero(live1);
   publish(0, n0);
   s << "    }\n    __syncthreads();\n    if (role == 0) {\n";
   complete(0, n0, true);
-  s << "    } else {\n";
+  s << "    }\n    if (role == 1) {\n";
   complete(n0, R, false);
   s << "    }\n    __syncthreads();\n  }\n}\n";
   return s.str();
@@ -592,8 +604,9 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
   const int capv = (jit_variant() >> 8) & 255;
   const int cap = capv == 0 ? 32 : capv == 255 ? 0 : capv;
   const bool fenced = !((jit_variant() >> 16) & 1);
-  // bits 17-18: inputs loaded ahead of their use (0: the default 1)
+  // bits 17-18: inputs loaded ahead of their use (0: the default 1); bit 21: serial XOR folds
   const int ahead = std::max(1, (jit_variant() >> 17) & 3);
+  const bool linear = (jit_variant() >> 21) & 1;
   const int tile = gfw_tile(W, R);  // the launch covers whole tiles only
   std::ostringstream s;
   gfw_prelude(s, R, K, W, 4096);
@@ -629,7 +642,7 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
     if (u + ahead < used.size()) load(u + ahead);
     const std::string e = "e" + std::to_string(u % nbuf);
     s << "    tr(" << e << ");\n";
-    gfw_net(s, mat, K, W, used[u], rows, acc, live, cap, e, "    ");
+    gfw_net(s, mat, K, W, used[u], rows, acc, live, cap, e, "    ", linear);
     if (fenced) s << "    __builtin_amdgcn_sched_barrier(0);\n";
   }
   for (int r = 0; r < R; ++r) {

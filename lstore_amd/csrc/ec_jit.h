@@ -26,7 +26,7 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int w);
 // bytes of a shard one block of an R-row w = 16 / 32 network covers per tile; it serves whole
 // tiles only
 int gfw_tile(int w, int R);
-// whether the R-row network at w takes the wave-pair row split (ec_jit.cpp)
+// whether the R-row network at w takes the wave-pair slice split (4 rows at w = 32; ec_jit.cpp)
 bool gfw_rowsplit(int w, int R);
 // bytes of a shard one 256-lane block of the network covers per tile
 int xornet_tile(int K);

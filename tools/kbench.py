@@ -22,6 +22,10 @@ CONFIGS = {
     "cg63": (L.CAUCHY_GOOD, 6, 3, 1 << 20),
     "cg104": (L.CAUCHY_GOOD, 10, 4, 4 << 20),
     "rs206": (L.REED_SOL_VAN, 20, 6, 256 << 10),
+    "rs104c4": (L.REED_SOL_VAN, 10, 4, 4 << 20),
+    "rs104c8": (L.REED_SOL_VAN, 10, 4, 8 << 20),
+    "cg124c4": (L.CAUCHY_GOOD, 12, 4, 4 << 20),
+    "cg124c8": (L.CAUCHY_GOOD, 12, 4, 8 << 20),
     "rs164": (L.REED_SOL_VAN, 16, 4, 1 << 20),
     "rs124": (L.REED_SOL_VAN, 12, 4, 1 << 20),
     "rs84": (L.REED_SOL_VAN, 8, 4, 1 << 20),
