@@ -81,8 +81,10 @@ bool jit_on() {
 
 bool wants_gfw_net(int R, int K, int w) {
   // every non-trivial w = 16 / 32 matrix (XOR-only ones take the plain-XOR path); at w = 32 the
-  // R x 32 accumulator slices limit a network to 4 rows, as the generic kernel's launches
-  return jit_on() && (w == 16 || w == 32) && R >= 1 && R <= (w == 32 ? 4 : kMaxRows) && K >= 1 && K <= kMaxCols;
+  // R x 32 accumulator slices limit the one-wave form to 4 rows, the wave-pair split (half the
+  // slices per wave) to 6 (8 rows spill at 2 waves per SIMD)
+  const int max_w32 = gfw_rowsplit(32, 4) ? 6 : 4;
+  return jit_on() && (w == 16 || w == 32) && R >= 1 && R <= (w == 32 ? max_w32 : kMaxRows) && K >= 1 && K <= kMaxCols;
 }
 
 bool wants_xornet(int R, int K) {
@@ -326,7 +328,9 @@ bool gfw_rowsplit(int w, int R) {
   // the wave-pair split below for 4-row networks at w = 32, where the one-wave form holds one
   // wave per SIMD (RS(10+4) encode 0.66 -> 0.76; at 3 rows the one-wave form holds two and the
   // split gains nothing: profiles/r04_v9_gfw_w32_split.txt).  LSEC_JIT_VARIANT bit 19 turns it off
-  return w == 32 && R >= 4 && !((jit_variant() >> 19) & 1);
+  if ((jit_variant() >> 19) & 1) return false;
+  // LSEC_JIT_VARIANT bit 24: also at w = 16 from 5 rows (A/B)
+  return (w == 32 && R >= 4) || (w == 16 && R >= 5 && ((jit_variant() >> 24) & 1));
 }
 
 int gfw_tile(int w, int R) { return gfw_rowsplit(w, R) ? 128 * 4 * w : 256 * 4 * w; }
@@ -453,15 +457,18 @@ std::vector<int> gfw_used(const uint32_t *mat, int R, int K) {
 // those in: every input is still loaded and transposed once and the accumulators halve (64 VGPRs
 // at 4 rows).  At the end the halves meet through LDS: role 0 transposes and stores rows
 // 0 .. ceil(R/2)-1, role 1 the rest.  Tile: 128 lane columns x 16 B x 8 pieces, 2 KiB apart
-// (16 KiB per shard); LDS 2 pairs x 2 roles x 8 KiB.  The roles' code sits in two consecutive
-// `if (role == r)` blocks, never in if / else: at an if / else join the compiler kept both
-// branches' accumulators apart (294 registers at RS(10+4) even with identical branches; 139 as
-// consecutive ifs, profiles/r04_v7_gfw_w32_ab.md).
+// (16 KiB per shard); LDS 2 pairs x 2 roles x 8 KiB (12 KiB at 5-6 rows).  The roles' code sits
+// in two consecutive `if (role == r)` blocks, never in if / else: at an if / else join the
+// compiler kept both branches' accumulators apart (294 registers at RS(10+4) even with identical
+// branches; 139 as consecutive ifs, profiles/r04_v9_gfw_w32_split.txt).
 std::string gfw_rowsplit_source(const uint32_t *mat, int R, int K, int W) {
   const int capv = (jit_variant() >> 8) & 255;
   const int cap = capv == 0 ? 32 : capv == 255 ? 0 : capv;
   const int tile = gfw_tile(W, R), HW = W / 2;
   const int n0 = (R + 1) / 2;  // output rows of role 0: 0 .. n0-1; role 1: n0 .. R-1
+  // quads (64 lanes x 16 B) of a wave's LDS slot: one transposed input (W / 4), or the half
+  // slices of the rows it hands its partner at the end (at most n0 rows of HW / 4)
+  const int lq = std::max(W / 4, n0 * (HW / 4));
   std::vector<int> rows;
   std::vector<std::string> acc;
   for (int r = 0; r < R; ++r) {
@@ -477,12 +484,12 @@ std::string gfw_rowsplit_source(const uint32_t *mat, int R, int K, int W) {
   // waves per SIMD for the register allocator (bits 22-23: 1 none, 2 four, 3 two), which RS(10+4)
   // meets at 167 registers without spills
   const bool linear = !((jit_variant() >> 21) & 1);
-  const int wv_opt = (jit_variant() >> 22) & 3, wpe = wv_opt == 0 ? 3 : wv_opt == 1 ? 0 : wv_opt == 2 ? 4 : 2;
+  const int wv_opt = (jit_variant() >> 22) & 3, wpe = wv_opt == 0 ? (R <= 4 ? 3 : 2) : wv_opt == 1 ? 0 : wv_opt == 2 ? 4 : 2;
   gfw_prelude(s, R, K, W, 128 * 16);
   s << "extern \"C\" __global__ __launch_bounds__(256) ";
   if (wpe) s << "__attribute__((amdgpu_waves_per_eu(" << wpe << "))) ";
   s << "void lsec_xornet(Args a) {\n"
-       "  __shared__ u32x4 L[2][2][W / 4][64];\n"
+    << "  __shared__ u32x4 L[2][2][" << lq << "][64];\n"
        "  const unsigned wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;\n"
        "  const unsigned pair = wv >> 1, role = wv & 1;\n"
        "  u32x4 (*const mine)[64] = L[pair][role];\n"

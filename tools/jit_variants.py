@@ -27,7 +27,7 @@ def main():
     M = np.array(O.coding_matrix(E.JE_METHOD_NAMES.index(a.method), k, m, a.w), dtype=np.int64).reshape(m, k)
     M &= (1 << a.w) - 1
     if a.w == 32:
-        M = M[:4]  # a network takes at most 4 rows at w = 32 (the encode binds all m rows)
+        M = M[:8]  # a network takes at most 8 rows (the encode binds all m rows)
     inp = f"{M.shape[0]} {k} {a.w} " + " ".join(map(str, M.flatten()))
     os.makedirs(os.path.join(ROOT, "build", "jit"), exist_ok=True)
     for v in a.variants.split(","):

@@ -35,6 +35,8 @@ CONFIGS = {
     "rs63w32": (L.REED_SOL_VAN, 6, 3, 1 << 20, 32),
     "rs104w16": (L.REED_SOL_VAN, 10, 4, 1 << 20, 16),
     "rs104w32": (L.REED_SOL_VAN, 10, 4, 1 << 20, 32),
+    "rs106w32": (L.REED_SOL_VAN, 10, 6, 1 << 20, 32),
+    "rs105w32": (L.REED_SOL_VAN, 10, 5, 1 << 20, 32),
     "rs206w16": (L.REED_SOL_VAN, 20, 6, 256 << 10, 16),
     "cg63w16": (L.CAUCHY_GOOD, 6, 3, 1 << 20, 16),
     "cg63w32": (L.CAUCHY_GOOD, 6, 3, 1 << 20, 32),
@@ -66,9 +68,10 @@ def main():
         plan.prepare_encode()  # wide codes: wait for the compiled XOR network (variant 0,0 uses it)
         plan.prepare_decode([0])
         import time
-        t_end = time.time() + 240  # heavy networks can take longer than prepare's 30 s wait
-        while time.time() < t_end and not plan.jit():  # (a lost-D0 decode may be XOR-only: no network)
-            time.sleep(1)
+        t_end = time.time() + 90  # heavy networks can take longer than prepare's 30 s wait (none may come:
+        while time.time() < t_end and not plan.jit():  # the plan may have no network at all)
+            time.sleep(5)
+            print(f"{name}: waiting for the encode network", flush=True)
         print(f"{name}: encode network {'ready' if plan.jit() else 'NOT ready'}", flush=True)
         plan.encode_dev(data, par)
         ref_par = par.clone()
