@@ -325,12 +325,12 @@ void share_slice_pairs(std::vector<std::vector<int>> &rows, int W, int cap, std:
 }  // namespace
 
 bool gfw_rowsplit(int w, int R) {
-  // the wave-pair split below for 4-row networks at w = 32, where the one-wave form holds one
+  // the wave-pair split below for networks of 4+ rows at w = 32, where the one-wave form holds one
   // wave per SIMD (RS(10+4) encode 0.66 -> 0.76; at 3 rows the one-wave form holds two and the
   // split gains nothing: profiles/r04_v9_gfw_w32_split.txt).  LSEC_JIT_VARIANT bit 19 turns it off
+  // and from 5 rows at w = 16 (RS(20+6) 0.68 -> 0.72; bit 24 turns that off)
   if ((jit_variant() >> 19) & 1) return false;
-  // LSEC_JIT_VARIANT bit 24: also at w = 16 from 5 rows (A/B)
-  return (w == 32 && R >= 4) || (w == 16 && R >= 5 && ((jit_variant() >> 24) & 1));
+  return (w == 32 && R >= 4) || (w == 16 && R >= 5 && !((jit_variant() >> 24) & 1));
 }
 
 int gfw_tile(int w, int R) { return gfw_rowsplit(w, R) ? 128 * 4 * w : 256 * 4 * w; }
@@ -447,7 +447,7 @@ std::vector<int> gfw_used(const uint32_t *mat, int R, int K) {
   return used;
 }
 
-// Wave-pair split of the w = 32 network.  The one-wave form keeps R x 32
+// Wave-pair split of the w = 32 (4-6 rows) and w = 16 (5-8 rows) networks.  The one-wave form keeps R x 32
 // accumulator slices per lane (128 VGPRs at 4 rows) plus two inputs' 32 slices: at 4 rows its code
 // object takes 273 registers, one wave per SIMD.  Here the 4 waves of a block form 2 pairs; the two waves of a pair cover the same 64 lane
 // columns and each computes half of every output row's bit slices (role 0 slices 0-15, role 1

@@ -444,6 +444,7 @@ def test_xor_network_vs_oracle(cuda, k, m, size):
     (L.REED_SOL_VAN, 7, 4, 32, 3 * 16384, [1, 7, 8, 10]),   # decode mixing data and coding losses
     (L.REED_SOL_VAN, 10, 6, 32, 2 * 16384 + 8, [0, 2, 4, 6, 8, 13]),  # 6 rows: the split's widest
     (L.REED_SOL_VAN, 9, 5, 32, 16384, [1, 3, 5, 9, 12]),   # 5 rows, odd input count
+    (L.REED_SOL_VAN, 19, 8, 16, 2 * 8192 + 16, [0, 2, 3, 7, 11, 18, 19, 26]),  # w = 16 split, 8 rows
 ])
 def test_gfw_network_vs_oracle(cuda, method, k, m, w, size, lost):
     """RS / r6 at w = 16 / 32 run on their compiled bit-sliced XOR networks (ec_jit.cpp,

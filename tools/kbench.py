@@ -38,6 +38,8 @@ CONFIGS = {
     "rs106w32": (L.REED_SOL_VAN, 10, 6, 1 << 20, 32),
     "rs105w32": (L.REED_SOL_VAN, 10, 5, 1 << 20, 32),
     "rs206w16": (L.REED_SOL_VAN, 20, 6, 256 << 10, 16),
+    "rs208w16": (L.REED_SOL_VAN, 20, 8, 256 << 10, 16),
+    "rs165w16": (L.REED_SOL_VAN, 16, 5, 1 << 20, 16),
     "cg63w16": (L.CAUCHY_GOOD, 6, 3, 1 << 20, 16),
     "cg63w32": (L.CAUCHY_GOOD, 6, 3, 1 << 20, 32),
 }
