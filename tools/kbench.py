@@ -70,8 +70,11 @@ def main():
         plan.prepare_encode()  # wide codes: wait for the compiled XOR network (variant 0,0 uses it)
         plan.prepare_decode([0])
         import time
-        t_end = time.time() + 90  # heavy networks can take longer than prepare's 30 s wait (none may come:
-        while time.time() < t_end and not plan.jit():  # the plan may have no network at all)
+        # heavy networks can take longer than prepare's 30 s wait; only codes that get one
+        # (ec_jit.cpp wants_xornet / wants_gfw_net: RS at w = 16 / 32, wide RS at w = 8)
+        has_net = meth == L.REED_SOL_VAN and (w in (16, 32) or m * k >= 96)
+        t_end = time.time() + (90 if has_net else 0)
+        while time.time() < t_end and not plan.jit():
             time.sleep(5)
             print(f"{name}: waiting for the encode network", flush=True)
         print(f"{name}: encode network {'ready' if plan.jit() else 'NOT ready'}", flush=True)
