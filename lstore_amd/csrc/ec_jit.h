@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include "ec_kernels.h"
 
@@ -37,6 +38,23 @@ int jit_variant();
 void bind(const void *image, const uint8_t *mat, int R, int K);
 void bind_w(const void *image, const uint32_t *mat, int R, int K, int w);  // w = 16 / 32
 void bind_entry(const void *image, const uint32_t *mat, int R, int K, int w);
+void bind_key(const void *image, const std::vector<uint32_t> &key, const uint32_t *mat, size_t n, int R, int K, int w,
+              int D);
+// whether an R-output bitmatrix code over K inputs at w is served by a packet network
+bool wants_pktnet(int R, int K, int w);
+// HIP source of the packet network for bitmatrix row masks [(r*w + l)*K + j] (w <= 32), D dwords
+// per lane (exposed for tests and tools)
+std::string pktnet_source(const uint32_t *masks, int R, int K, int w, int D);
+// bind a bitmatrix image (ungrouped row masks, K <= 16) to its packet network; the lane width
+// follows the packet size
+void bind_pkt(const void *image, const uint32_t *masks, int R, int K, int w, int packet);
+// out[r] packets = the bitmatrix rows' XORs of the input packets, every stripe; the shard bases
+// and strides must be aligned to the lane width (pkt_aligned)
+hipError_t launch_pkt(hipFunction_t fn, int R, int K, const ShardRef *in, const ShardRef *out, int nstripes, int64_t size,
+                      int packet, int w, hipStream_t st);
+// dwords per lane of the packet network for R outputs at w with this packet size (0: none)
+int pkt_dwords(int R, int w, int packet);
+bool pkt_aligned(const ShardRef *in, int K, const ShardRef *out, int R, int w, int packet);
 void unbind(const void *image);
 // Block until the image's network is compiled (or failed, or timeout): 1 ready, 0 otherwise
 // (also 0 when the image has no network).

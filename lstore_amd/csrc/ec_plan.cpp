@@ -379,6 +379,8 @@ int encode_cells_locked(PlanExt *e, int dev, const void **out) {
       it = e->impl->enc_dev_masks.emplace(dev, d).first;
       if (kernel_kind(e->pub.method, e->pub.w) == KWORDWISE)  // RS / r6 at w = 16 / 32: a bit-sliced network
         lsec::jit::bind_w(d, e->impl->coding_w.data(), encode_rows(e), e->pub.data_strips, e->pub.w);
+      else if (kernel_kind(e->pub.method, e->pub.w) == KBITMATRIX)  // liberation family: a packet network
+        lsec::jit::bind_pkt(d, e->impl->enc_masks.data(), encode_rows(e), e->pub.data_strips, e->pub.w, e->pub.packet_size);
     }
     *out = it->second;
     return 0;
@@ -504,6 +506,9 @@ int decode_entry_locked(PlanExt *e, const std::vector<int> &ids, int dev, Decode
       dm = ent.dev_masks.emplace(dev, d).first;
       if (kind == KWORDWISE)
         lsec::jit::bind_w(d, ent.wrows.data(), static_cast<int>(ent.dp.erased.size()), e->pub.data_strips, e->pub.w);
+      else if (kind == KBITMATRIX)
+        lsec::jit::bind_pkt(d, ent.masks.data(), static_cast<int>(ent.dp.erased.size()), e->pub.data_strips, e->pub.w,
+                            e->pub.packet_size);
     }
     *out = &ent;
     *cells = dm->second;
@@ -583,6 +588,13 @@ int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in,
       size -= whole;
     }
   }
+  if (kind == KBITMATRIX && lsec::bitsliced_variant() == 0 && lsec::jit::wants_pktnet(R, K, w) &&
+      lsec::jit::pkt_aligned(in, K, out, R, w, packet))
+    if (hipFunction_t fn = lsec::jit::ready(image, R, K)) {  // the bitmatrix's compiled packet network
+      const hipError_t err = lsec::jit::launch_pkt(fn, R, K, in, out, nstripes, size, packet, w, st);
+      if (err != hipSuccess) return fail("packet network launch failed: %s", hipGetErrorString(err));
+      return 0;
+    }
   const int rmax = kind == KBITMATRIX ? 2 : ((kind == KBITSLICEDW || kind == KWORDWISE) && w == 32) ? 4 : 8;
   const int rpr = image_rows_per_output(kind, w), unit = image_unit(kind, w);
   // input groups of at most kMaxK (grouped image layout); groups after the first accumulate
@@ -1042,7 +1054,8 @@ int lsec_plan_jit(lio_erasure_plan_t *plan, const int *erasures) {
   PlanExt *e = ext_of(plan);
   if (!e) return 0;
   const int kind = kernel_kind(e->pub.method, e->pub.w);
-  if (kind == KBYTEWISE ? lsec::bytewise_variant() != 0 : kind == KWORDWISE ? lsec::bitsliced_variant() != 0 : true)
+  if (kind == KBYTEWISE ? lsec::bytewise_variant() != 0
+                        : (kind == KWORDWISE || kind == KBITMATRIX) ? lsec::bitsliced_variant() != 0 : true)
     return 0;
   const void *cells = nullptr;
   int R = 0;
@@ -1057,7 +1070,6 @@ int lsec_plan_jit(lio_erasure_plan_t *plan, const int *erasures) {
   }
   return lsec::jit::ready(cells, R, plan->data_strips) != nullptr ? 1 : 0;
 }
-
 
 int lsec_plan_kernel(lio_erasure_plan_t *plan) { return plan ? kernel_kind(plan->method, plan->w) : 0; }
 

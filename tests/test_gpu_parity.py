@@ -95,6 +95,51 @@ def test_liberation_family_vs_reference(cuda, method, k, w):
             assert np.array_equal(sh, full), er
 
 
+@pytest.mark.parametrize("method,k,w,P,nsuper", [
+    (L.LIBERATION, 6, 7, 32, 40),     # 16 B lanes; 40 super-packets: a ragged last column tile
+    (L.LIBERATION, 7, 7, 40, 33),     # P % 16 == 8: 8 B lanes
+    (L.BLAUM_ROTH, 6, 6, 24, 50),     # (Jerasure packets are whole longs: P % 8 == 0)
+    (L.LIBER8TION, 8, 8, 64, 24),
+    (L.LIBER8TION, 3, 8, 16, 70),
+    (L.BLAUM_ROTH, 16, 16, 32, 12),   # R*w = 32: 8 B lanes by the register cap
+])
+def test_bitmatrix_network_vs_reference(cuda, method, k, w, P, nsuper):
+    """Liberation-family codes on their compiled packet networks (ec_jit.cpp pktnet_source) once
+    prepared: encode bit-exact vs the real reference (oracle/_ref), device-resident over three
+    stripes and from host memory, and decodes of data, coding and mixed losses (double losses on
+    a network) back to the encoded bytes (the MDS code's recovered bytes are unique)."""
+    import torch
+
+    if not O.ref_available():
+        pytest.skip("oracle/_ref not built")
+    m, n = 2, 3
+    size = w * P * nsuper
+    rng = np.random.default_rng(k * w + P)
+    data = rng.integers(0, 256, (n, k, size), dtype=np.uint8)
+    data[1] = 0xFF
+    rp = O.RefPlan(method, k, m, w, P)
+    want = np.stack([rp.encode(data[s]) for s in range(n)])
+    losses = ([0], [k - 1], [k], [k + 1], [0, k - 1], [1, k], [k, k + 1])
+    with L.Plan.new(method, size, k, m, w, P, 8) as p:
+        assert p.form_encoding_matrix() == 0 and p.form_decoding_matrix() == 0
+        p.prepare_encode()
+        assert p.jit() == 1, "packet network not compiled"
+        par = torch.full((n, m, size), 0x5A, dtype=torch.uint8, device="cuda")
+        p.encode_dev(torch.from_numpy(data.copy()).cuda(), par)
+        assert np.array_equal(par.cpu().numpy(), want)
+        host = np.concatenate([data, np.zeros((n, m, size), np.uint8)], axis=1)
+        p.encode_stripes(host)
+        assert np.array_equal(host[:, k:], want)
+        for er in losses:
+            p.prepare_decode(er)
+            if len(er) == 2 and er[0] < k:  # two outputs on a network (single erasures: k_bitmatrix)
+                assert p.jit(er) == 1, er
+            sh = host.copy()
+            sh[:, er] = 0x33
+            p.decode_stripes(sh, er)
+            assert_same(sh, host)
+
+
 @pytest.mark.parametrize("k", [128, 252])
 def test_wide_liberation_decodes_round_trip(cuda, k):
     """Liberation with k = 128 (w = 131) and k = 252 (k + m = 254, w = nearest_prime(252) = 257

@@ -41,6 +41,14 @@ CONFIGS = {
     "rs208w16": (L.REED_SOL_VAN, 20, 8, 256 << 10, 16),
     "rs165w16": (L.REED_SOL_VAN, 16, 5, 1 << 20, 16),
     "cg63w16": (L.CAUCHY_GOOD, 6, 3, 1 << 20, 16),
+    "cg104w16": (L.CAUCHY_GOOD, 10, 4, 1 << 20, 16),
+    "cg104w32": (L.CAUCHY_GOOD, 10, 4, 1 << 20, 32),
+    # bitmatrix codes (K3): liberation w = 7, Blaum-Roth w = 6, liber8tion w = 8, raid4, r6
+    "lib62": (L.LIBERATION, 6, 2, 7 << 17, 7),
+    "br62": (L.BLAUM_ROTH, 6, 2, 6 << 17, 6),
+    "l8t62": (L.LIBER8TION, 6, 2, 1 << 20, 8),
+    "raid4_6": (L.RAID4, 6, 1, 1 << 20),
+    "r6_62": (L.REED_SOL_R6_OP, 6, 2, 1 << 20),
     "cg63w32": (L.CAUCHY_GOOD, 6, 3, 1 << 20, 32),
 }
 
