@@ -36,6 +36,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -91,7 +92,7 @@ bool wants_pktnet(int R, int K, int w) {
   // liberation-family bitmatrices (one mask word per bit-row and input) of modest width, two
   // outputs (encodes, double erasures): single-erasure decodes measured 0.72 on a network against
   // 0.76 on k_bitmatrix (profiles/r04_v12_pktnet.txt)
-  return jit_on() && w >= 2 && w <= 32 && R >= 2 && R <= kMaxRows && K >= 1 && K <= 16 && R * w <= 64;
+  return jit_on() && w >= 2 && w <= 32 && R >= 2 && R <= kMaxRows && K >= 1 && K <= 16 && R * w <= 256;
 }
 
 bool wants_xornet(int R, int K) {
@@ -611,14 +612,19 @@ std::string gfw_rowsplit_source(const uint32_t *mat, int R, int K, int W) {
 }  // namespace
 
 // Packet networks for bitmatrix codes (liberation / blaum_roth / liber8tion; jerasure_bitmatrix_dotprod,
-// jerasure.c:317-362): a super-packet is w packets of P bytes per shard; packet l of output r is
-// the XOR of the input packets (j, x) whose bit B[r*w+l][j*w+x] is set.  With the bitmatrix known
-// when the kernel is compiled every output packet is a straight XOR chain (shared pairs per input,
-// as gfw_net), where k_bitmatrix tests R*w*w mask bits per input under uniform branches and moves
-// 4 B per lane.  A lane owns D dwords (16 B at P % 16 == 0) of one packet column: it loads the w
-// packets of that column of each input (one input ahead, fenced), and stores R*w packets.
+// jerasure.c:317-362) and for Cauchy codes at w = 16 / 32 (the bitmatrix of each GF(2^w)
+// coefficient): a super-packet is w packets of P bytes per shard; packet l of output r is the XOR
+// of the input packets (j, x) whose bit B[r*w+l][j*w+x] is set.  With the bitmatrix known when the
+// kernel is compiled every output packet is a straight XOR chain (shared pairs per input, as
+// gfw_net), where k_bitmatrix tests R*w*w mask bits per input under uniform branches and moves 4 B
+// per lane, and k_gfw_bitsliced XORs w slices per set coefficient bit.  A lane owns D dwords (16 B
+// at P % 16 == 0) of one packet column; it loads the packets of that column each input needs (one
+// input ahead, fenced) and stores its output packets.  With S > 1 groups (an A/B knob; slower)
+// the output packets (r, l) are split by l into S groups, tile t computing group t % S of column
+// tile t / S: the groups of one column run side by side on one XCD and re-read the inputs from its
+// L2.  Lanes past the last column redo the last column: no divergent branch.
 // masks[((r*w + l)*K + j)] bit x = B[r*w+l][j*w+x] (w <= 32).
-std::string pktnet_source(const uint32_t *masks, int R, int K, int W, int D) {
+std::string pktnet_source(const uint32_t *masks, int R, int K, int W, int D, int S) {
   const int capv = (jit_variant() >> 8) & 255;
   const int cap = capv == 0 ? 32 : capv == 255 ? 0 : capv;
   const int tile = 256 * 4 * D;
@@ -647,65 +653,86 @@ std::string pktnet_source(const uint32_t *masks, int R, int K, int W, int D) {
        "  const unsigned P = (unsigned)a.packet;\n"
     << "  const unsigned cols = (unsigned)(a.size / " << W << ");\n"
     << "  const unsigned tps = (cols + " << tile - 1 << ") / " << tile << ";\n"
-       "  const unsigned nt = tps * (unsigned)a.nstripes;\n"
+    << "  const unsigned nt = tps * (unsigned)a.nstripes * " << S << "u;\n"
        "  const unsigned nb = gridDim.x, per = nb >> 3, rem = nb & 7, xcd = blockIdx.x & 7;\n"
        "  const unsigned t0 = xcd * per + (xcd < rem ? xcd : rem) + (blockIdx.x >> 3);\n"
        "  for (unsigned t = t0; t < nt; t += nb) {\n"
-       "    const unsigned s = t / tps;\n"
-    << "    const unsigned colb = (t - s * tps) * " << tile << " + threadIdx.x * " << 4 * D << ";\n"
-       "    if (colb >= cols) continue;\n"
+    << "    const unsigned g = t % " << S << "u, ct = t / " << S << "u;\n"
+       "    const unsigned s = ct / tps;\n"
+    // lanes past the last column redo the last column (same loads, same bytes stored)
+    << "    const unsigned colb = min((ct - s * tps) * " << tile << " + threadIdx.x * " << 4 * D << ", cols - " << 4 * D << "u);\n"
        "    const unsigned sp = colb / P;\n"
     << "    const long long off = (long long)sp * " << W << " * P + (colb - sp * P);\n";
+  const int per_g = (W + S - 1) / S;
+  // accumulators and input buffers declared once, shared by the groups' blocks (each group's
+  // packet l uses slot l - l0): the compiler then gives the blocks the same registers
   for (int r = 0; r < R; ++r)
-    for (int l = 0; l < W; ++l) s << "    u32 h" << r << "_" << l << "[D];\n";
-  std::vector<std::vector<bool>> live(static_cast<size_t>(R) * W, std::vector<bool>(1, false));
-  std::vector<int> used;
-  for (int j = 0; j < K; ++j) {
-    bool any = false;
-    for (int r = 0; r < R * W && !any; ++r) any = masks[static_cast<size_t>(r) * K + j] != 0;
-    if (any) used.push_back(j);
-  }
-  auto load = [&](size_t u) {
-    const int j = used[u];
-    s << "    { const unsigned long long p = a.in[" << j << "].base + (unsigned long long)s * a.in[" << j
-      << "].stride + off;\n";
-    for (int x = 0; x < W; ++x) s << "      ld(e" << u % 2 << "_" << x << ", p + " << x << "ull * P);\n";
-    s << "    }\n";
-  };
-  for (int b = 0; b < 2; ++b)
-    for (int x = 0; x < W; ++x) s << "    u32 e" << b << "_" << x << "[D];\n";
-  if (!used.empty()) load(0);
-  for (size_t u = 0; u < used.size(); ++u) {
-    const int j = used[u];
-    if (u + 1 < used.size()) load(u + 1);
-    std::vector<std::vector<int>> rows(static_cast<size_t>(R) * W);
-    for (int rl = 0; rl < R * W; ++rl) {
-      const uint32_t m = masks[static_cast<size_t>(rl) * K + j];
+    for (int i = 0; i < per_g; ++i) s << "    u32 h" << r << "_" << i << "[D];\n";
+  for (int b2 = 0; b2 < 2; ++b2)
+    for (int x = 0; x < W; ++x) s << "    u32 e" << b2 << "_" << x << "[D];\n";
+  for (int grp = 0; grp < S; ++grp) {
+    const int l0 = grp * per_g, l1 = std::min(W, l0 + per_g);
+    if (l0 >= l1) continue;
+    std::vector<int> rl_of;  // this group's output packets, as r*W + l
+    for (int r = 0; r < R; ++r)
+      for (int l = l0; l < l1; ++l) rl_of.push_back(r * W + l);
+    s << "    if (g == " << grp << "u) {\n";
+    std::vector<bool> live(static_cast<size_t>(R) * W, false);
+    // inputs and their packets this group reads
+    std::vector<int> used;
+    std::vector<uint32_t> need;
+    for (int j = 0; j < K; ++j) {
+      uint32_t nm_ = 0;
+      for (int rl : rl_of) nm_ |= masks[static_cast<size_t>(rl) * K + j];
+      if (nm_) {
+        used.push_back(j);
+        need.push_back(nm_);
+      }
+    }
+    auto load = [&](size_t u) {
+      const int j = used[u];
+      s << "      { const unsigned long long p = a.in[" << j << "].base + (unsigned long long)s * a.in[" << j
+        << "].stride + off;\n";
       for (int x = 0; x < W; ++x)
-        if ((m >> x) & 1u) rows[rl].push_back(x);
+        if ((need[u] >> x) & 1u) s << "        ld(e" << u % 2 << "_" << x << ", p + " << x << "ull * P);\n";
+      s << "      }\n";
+    };
+    if (!used.empty()) load(0);
+    for (size_t u = 0; u < used.size(); ++u) {
+      const int j = used[u];
+      if (u + 1 < used.size()) load(u + 1);
+      std::vector<std::vector<int>> rows(rl_of.size());
+      for (size_t i = 0; i < rl_of.size(); ++i) {
+        const uint32_t m = masks[static_cast<size_t>(rl_of[i]) * K + j];
+        for (int x = 0; x < W; ++x)
+          if ((m >> x) & 1u) rows[i].push_back(x);
+      }
+      std::vector<std::pair<int, int>> pairs;
+      if (cap > 0) share_slice_pairs(rows, W, cap, pairs);
+      const std::string eb = "e" + std::to_string(u % 2) + "_";
+      auto nm = [&](int x) { return x < W ? eb + std::to_string(x) + "[d]" : "p" + std::to_string(x - W); };
+      s << "      for (int d = 0; d < D; ++d) {\n";
+      for (size_t i = 0; i < pairs.size(); ++i)
+        s << "        const u32 p" << i << " = " << nm(pairs[i].first) << " ^ " << nm(pairs[i].second) << ";\n";
+      for (size_t i = 0; i < rl_of.size(); ++i) {
+        if (rows[i].empty()) continue;
+        const int rl = rl_of[i];
+        const std::string acc = "h" + std::to_string(rl / W) + "_" + std::to_string(rl % W - l0) + "[d]";
+        std::vector<std::string> t;
+        if (live[rl]) t.push_back(acc);
+        for (int x : rows[i]) t.push_back(nm(x));
+        s << "        " << acc << " = " << xor_chain(t) << ";\n";
+        live[rl] = true;
+      }
+      s << "      }\n      __builtin_amdgcn_sched_barrier(0);\n";
     }
-    std::vector<std::pair<int, int>> pairs;
-    if (cap > 0) share_slice_pairs(rows, W, cap, pairs);
-    const std::string eb = "e" + std::to_string(u % 2) + "_";
-    auto nm = [&](int x) { return x < W ? eb + std::to_string(x) + "[d]" : "p" + std::to_string(x - W); };
-    s << "    for (int d = 0; d < D; ++d) {\n";
-    for (size_t i = 0; i < pairs.size(); ++i) s << "      const u32 p" << i << " = " << nm(pairs[i].first) << " ^ " << nm(pairs[i].second) << ";\n";
-    for (int rl = 0; rl < R * W; ++rl) {
-      if (rows[rl].empty()) continue;
-      const std::string acc = "h" + std::to_string(rl / W) + "_" + std::to_string(rl % W) + "[d]";
-      std::vector<std::string> t;
-      if (live[rl][0]) t.push_back(acc);
-      for (int x : rows[rl]) t.push_back(nm(x));
-      s << "      " << acc << " = " << xor_chain(t) << ";\n";
-      live[rl][0] = true;
-    }
-    s << "    }\n    __builtin_amdgcn_sched_barrier(0);\n";
-  }
-  for (int r = 0; r < R; ++r) {
-    s << "    { const unsigned long long q = a.out[" << r << "].base + (unsigned long long)s * a.out[" << r << "].stride + off;\n";
-    for (int l = 0; l < W; ++l) {
-      if (!live[static_cast<size_t>(r) * W + l][0]) s << "      for (int d = 0; d < D; ++d) h" << r << "_" << l << "[d] = 0u;\n";
-      s << "      st(h" << r << "_" << l << ", q + " << l << "ull * P);\n";
+    for (int r = 0; r < R; ++r) {
+      s << "      { const unsigned long long q = a.out[" << r << "].base + (unsigned long long)s * a.out[" << r << "].stride + off;\n";
+      for (int l = l0; l < l1; ++l) {
+        if (!live[static_cast<size_t>(r) * W + l]) s << "        for (int d = 0; d < D; ++d) h" << r << "_" << l - l0 << "[d] = 0u;\n";
+        s << "        st(h" << r << "_" << l - l0 << ", q + " << l << "ull * P);\n";
+      }
+      s << "      }\n";
     }
     s << "    }\n";
   }
@@ -785,6 +812,7 @@ struct Entry {
   std::vector<uint32_t> mat;  // R x K coefficients (GF(2^w) elements)
   int R = 0, K = 0, w = 8;
   int D = 0;  // packet networks (pktnet_source): dwords per lane per packet; 0 = a matrix network
+  int S = 1;  // packet networks: output groups
   enum State { kCompiling, kReady, kFailed } state = kCompiling;
   std::vector<char> code;                 // code object
   std::map<int, hipModule_t> modules;     // device -> module
@@ -792,17 +820,25 @@ struct Entry {
   std::string err;
 };
 
-// leaked on purpose: a compile thread still running when the process exits may touch them
+// leaked on purpose: a compile still running when the process exits may touch them
 std::mutex &g_mu = *new std::mutex();
 std::condition_variable &g_cv = *new std::condition_variable();
-int g_compiling = 0;  // compile threads still running (waited for at exit, below)
+// Compiles run on at most kWorkers threads fed from a queue.  hipRTC's compiler keeps global
+// state that the process's exit destroys, so a compile may not still run then: at exit no queued
+// compile starts and the running ones are waited for (a thread per network, as before, left a
+// dozen compiling at the end of a test run: heap corruption at exit).
+constexpr int kWorkers = 2;
+auto &g_queue = *new std::deque<std::shared_ptr<struct Entry>>();
+int g_running = 0, g_workers = 0;
+bool g_exiting = false;
 // bumped whenever an image is bound or unbound: invalidates the threads' ready() caches
 std::atomic<uint64_t> g_gen{1};
 
-// at exit: give running compiles a short while to finish (they touch only leaked state)
 void drain_compiles() {
   std::unique_lock<std::mutex> lk(g_mu);
-  g_cv.wait_for(lk, std::chrono::seconds(2), [] { return g_compiling == 0; });
+  g_exiting = true;
+  g_cv.notify_all();
+  g_cv.wait_for(lk, std::chrono::seconds(120), [] { return g_running == 0; });
 }
 auto &g_by_matrix = *new std::map<std::vector<uint32_t>, std::shared_ptr<Entry>>();  // key: R, K, w, matrix
 auto &g_by_image = *new std::map<const void *, std::shared_ptr<Entry>>();           // device image -> entry
@@ -820,7 +856,7 @@ void compile(std::shared_ptr<Entry> e) {
   const auto t0 = std::chrono::steady_clock::now();
   std::string src;
   if (e->D > 0) {
-    src = pktnet_source(e->mat.data(), e->R, e->K, e->w, e->D);
+    src = pktnet_source(e->mat.data(), e->R, e->K, e->w, e->D, e->S);
   } else if (e->w == 8) {
     std::vector<uint8_t> m8(e->mat.begin(), e->mat.end());
     src = xornet_source(m8.data(), e->R, e->K);
@@ -856,8 +892,23 @@ void compile(std::shared_ptr<Entry> e) {
   e->code.swap(code);
   e->err = err;
   e->state = err.empty() ? Entry::kReady : Entry::kFailed;
-  --g_compiling;
+  --g_running;
   g_cv.notify_all();
+}
+
+void compile_worker() {
+  for (;;) {
+    std::shared_ptr<Entry> e;
+    {
+      std::unique_lock<std::mutex> lk(g_mu);
+      g_cv.wait(lk, [] { return g_exiting || !g_queue.empty(); });
+      if (g_exiting) return;
+      e = g_queue.front();
+      g_queue.pop_front();
+      ++g_running;
+    }
+    compile(e);
+  }
 }
 
 // the kernel of a ready entry on device `dev` (loads the module once per device; under g_mu)
@@ -892,22 +943,40 @@ void bind_w(const void *image, const uint32_t *mat, int R, int K, int w) {
 }
 
 void bind_entry(const void *image, const uint32_t *mat, int R, int K, int w) {
-  bind_key(image, key_of(mat, R, K, w), mat, static_cast<size_t>(R) * K, R, K, w, 0);
+  bind_key(image, key_of(mat, R, K, w), mat, static_cast<size_t>(R) * K, R, K, w, 0, 1);
 }
 
 void bind_pkt(const void *image, const uint32_t *masks, int R, int K, int w, int packet) {
   if (!image || !wants_pktnet(R, K, w)) return;
-  const int D = pkt_dwords(R, w, packet);
+  int D = 0, S = 1;
+  pkt_shape(R, w, packet, &D, &S);
   if (D == 0) return;
   const size_t n = static_cast<size_t>(R) * w * K;  // one mask word per (bit-row, input): w <= 32
   std::vector<uint32_t> key = {static_cast<uint32_t>(R), static_cast<uint32_t>(K), 1000u + static_cast<uint32_t>(w),
-                               static_cast<uint32_t>(D)};
+                               static_cast<uint32_t>(D), static_cast<uint32_t>(S)};
   key.insert(key.end(), masks, masks + n);
-  bind_key(image, key, masks, n, R, K, w, D);
+  bind_key(image, key, masks, n, R, K, w, D, S);
+}
+
+void bind_pkt_field(const void *image, const uint32_t *coef, int R, int K, int w, int packet) {
+  // the bitmatrix of each GF(2^w) coefficient: output packet l takes input packet x where bit l
+  // of c * x^x is set (Cauchy's packet layout, k_gfw_bitsliced)
+  if (!image || !wants_pktnet(R, K, w) || (w != 16 && w != 32)) return;
+  std::vector<uint32_t> masks(static_cast<size_t>(R) * w * K, 0u);
+  for (int r = 0; r < R; ++r)
+    for (int j = 0; j < K; ++j) {
+      uint32_t cx = coef[r * K + j] & (w == 16 ? 0xFFFFu : 0xFFFFFFFFu);
+      for (int x = 0; x < w && cx; ++x) {
+        for (int l = 0; l < w; ++l)
+          if ((cx >> l) & 1u) masks[(static_cast<size_t>(r) * w + l) * K + j] |= 1u << x;
+        cx = gfw_times_x(cx, w);
+      }
+    }
+  bind_pkt(image, masks.data(), R, K, w, packet);
 }
 
 void bind_key(const void *image, const std::vector<uint32_t> &key, const uint32_t *mat, size_t n, int R, int K, int w,
-              int D) {
+              int D, int S) {
   std::shared_ptr<Entry> e;
   bool start = false;
   {
@@ -920,9 +989,14 @@ void bind_key(const void *image, const std::vector<uint32_t> &key, const uint32_
       e->K = K;
       e->w = w;
       e->D = D;
+      e->S = S;
       g_by_matrix.emplace(key, e);
       start = true;
-      ++g_compiling;
+      g_queue.push_back(e);
+      if (g_workers < kWorkers) {
+        ++g_workers;
+        std::thread(compile_worker).detach();
+      }
       static std::once_flag once;
       std::call_once(once, [] { atexit(drain_compiles); });
     } else {
@@ -931,7 +1005,7 @@ void bind_key(const void *image, const std::vector<uint32_t> &key, const uint32_
     g_by_image[image] = e;
     g_gen.fetch_add(1, std::memory_order_acq_rel);
   }
-  if (start) std::thread(compile, e).detach();
+  if (start) g_cv.notify_all();
 }
 
 void unbind(const void *image) {
@@ -1007,25 +1081,30 @@ hipError_t launch_pkt(hipFunction_t fn, int R, int K, const ShardRef *in, const 
   std::memcpy(args.data() + 16 + sizeof(ShardRef) * K, out, sizeof(ShardRef) * R);
   size_t bytes = args.size();
   void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes, HIP_LAUNCH_PARAM_END};
-  const int D = pkt_dwords(R, w, packet);  // as bind_pkt
+  int D = 0, S = 1;
+  pkt_shape(R, w, packet, &D, &S);  // as bind_pkt
   const int64_t tile = 256 * 4 * D, cols = size / w;  // column bytes of a stripe: nsuper * packet
-  const uint64_t ntiles = static_cast<uint64_t>((cols + tile - 1) / tile) * static_cast<uint64_t>(nstripes);
+  const uint64_t ntiles = static_cast<uint64_t>((cols + tile - 1) / tile) * static_cast<uint64_t>(nstripes) * S;
   if (ntiles == 0) return hipSuccess;
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   return hipModuleLaunchKernel(fn, static_cast<unsigned>(ntiles), 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
 }
 
-int pkt_dwords(int R, int w, int packet) {
-  // 16 B per lane where the packet allows, fewer where R*w accumulator packets would exceed 64
-  // dwords (W = 7 / 8 at R = 2: 4 dwords, ~120 registers)
-  const int by_packet = packet % 16 == 0 ? 4 : packet % 8 == 0 ? 2 : packet % 4 == 0 ? 1 : 0;
-  int d = by_packet;
+void pkt_shape(int R, int w, int packet, int *D, int *S) {
+  // 16 B per lane where the packet allows, fewer where the R*w accumulator packets would pass 64
+  // dwords (w = 7 / 8 at R = 2: 4 dwords, ~120 registers).  One output group: Cauchy(10+4) at
+  // w = 32 (128 accumulators, one wave per SIMD) encodes at 0.80 that way, 0.61 / 0.41 in 2 / 4
+  // groups (profiles/r04_v13_pktnet_cauchy.txt); LSEC_JIT_VARIANT bits 25-26 force 1 / 2 / 4
+  int d = packet % 16 == 0 ? 4 : packet % 8 == 0 ? 2 : packet % 4 == 0 ? 1 : 0;
   while (d > 1 && R * w * d > 64) d /= 2;
-  return d;
+  const int fv = (jit_variant() >> 25) & 3;
+  *D = d;
+  *S = fv ? 1 << (fv - 1) : 1;
 }
 
 bool pkt_aligned(const ShardRef *in, int K, const ShardRef *out, int R, int w, int packet) {
-  const int d = pkt_dwords(R, w, packet);
+  int d = 0, g = 1;
+  pkt_shape(R, w, packet, &d, &g);
   if (d == 0) return false;
   const uint64_t a = 4u * static_cast<uint64_t>(d);
   for (int j = 0; j < K; ++j)

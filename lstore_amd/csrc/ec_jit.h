@@ -39,21 +39,23 @@ void bind(const void *image, const uint8_t *mat, int R, int K);
 void bind_w(const void *image, const uint32_t *mat, int R, int K, int w);  // w = 16 / 32
 void bind_entry(const void *image, const uint32_t *mat, int R, int K, int w);
 void bind_key(const void *image, const std::vector<uint32_t> &key, const uint32_t *mat, size_t n, int R, int K, int w,
-              int D);
+              int D, int S);
 // whether an R-output bitmatrix code over K inputs at w is served by a packet network
 bool wants_pktnet(int R, int K, int w);
 // HIP source of the packet network for bitmatrix row masks [(r*w + l)*K + j] (w <= 32), D dwords
 // per lane (exposed for tests and tools)
-std::string pktnet_source(const uint32_t *masks, int R, int K, int w, int D);
+std::string pktnet_source(const uint32_t *masks, int R, int K, int w, int D, int S = 1);
 // bind a bitmatrix image (ungrouped row masks, K <= 16) to its packet network; the lane width
 // follows the packet size
 void bind_pkt(const void *image, const uint32_t *masks, int R, int K, int w, int packet);
+// the same for an R x K GF(2^w) coefficient matrix in Cauchy's packet layout (w = 16 / 32)
+void bind_pkt_field(const void *image, const uint32_t *coef, int R, int K, int w, int packet);
 // out[r] packets = the bitmatrix rows' XORs of the input packets, every stripe; the shard bases
 // and strides must be aligned to the lane width (pkt_aligned)
 hipError_t launch_pkt(hipFunction_t fn, int R, int K, const ShardRef *in, const ShardRef *out, int nstripes, int64_t size,
                       int packet, int w, hipStream_t st);
-// dwords per lane of the packet network for R outputs at w with this packet size (0: none)
-int pkt_dwords(int R, int w, int packet);
+// lane width (dwords, 0: none) and output groups of the packet network for R outputs at w
+void pkt_shape(int R, int w, int packet, int *D, int *S);
 bool pkt_aligned(const ShardRef *in, int K, const ShardRef *out, int R, int w, int packet);
 void unbind(const void *image);
 // Block until the image's network is compiled (or failed, or timeout): 1 ready, 0 otherwise

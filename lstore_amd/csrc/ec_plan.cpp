@@ -381,6 +381,9 @@ int encode_cells_locked(PlanExt *e, int dev, const void **out) {
         lsec::jit::bind_w(d, e->impl->coding_w.data(), encode_rows(e), e->pub.data_strips, e->pub.w);
       else if (kernel_kind(e->pub.method, e->pub.w) == KBITMATRIX)  // liberation family: a packet network
         lsec::jit::bind_pkt(d, e->impl->enc_masks.data(), encode_rows(e), e->pub.data_strips, e->pub.w, e->pub.packet_size);
+      else if (kernel_kind(e->pub.method, e->pub.w) == KBITSLICEDW)  // Cauchy at w = 16 / 32: the same
+        lsec::jit::bind_pkt_field(d, e->impl->coding_w.data(), encode_rows(e), e->pub.data_strips, e->pub.w,
+                                  e->pub.packet_size);
     }
     *out = it->second;
     return 0;
@@ -509,6 +512,9 @@ int decode_entry_locked(PlanExt *e, const std::vector<int> &ids, int dev, Decode
       else if (kind == KBITMATRIX)
         lsec::jit::bind_pkt(d, ent.masks.data(), static_cast<int>(ent.dp.erased.size()), e->pub.data_strips, e->pub.w,
                             e->pub.packet_size);
+      else if (kind == KBITSLICEDW)
+        lsec::jit::bind_pkt_field(d, ent.wrows.data(), static_cast<int>(ent.dp.erased.size()), e->pub.data_strips,
+                                  e->pub.w, e->pub.packet_size);
     }
     *out = &ent;
     *cells = dm->second;
@@ -588,7 +594,7 @@ int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in,
       size -= whole;
     }
   }
-  if (kind == KBITMATRIX && lsec::bitsliced_variant() == 0 && lsec::jit::wants_pktnet(R, K, w) &&
+  if ((kind == KBITMATRIX || kind == KBITSLICEDW) && lsec::bitsliced_variant() == 0 && lsec::jit::wants_pktnet(R, K, w) &&
       lsec::jit::pkt_aligned(in, K, out, R, w, packet))
     if (hipFunction_t fn = lsec::jit::ready(image, R, K)) {  // the bitmatrix's compiled packet network
       const hipError_t err = lsec::jit::launch_pkt(fn, R, K, in, out, nstripes, size, packet, w, st);
@@ -1055,7 +1061,8 @@ int lsec_plan_jit(lio_erasure_plan_t *plan, const int *erasures) {
   if (!e) return 0;
   const int kind = kernel_kind(e->pub.method, e->pub.w);
   if (kind == KBYTEWISE ? lsec::bytewise_variant() != 0
-                        : (kind == KWORDWISE || kind == KBITMATRIX) ? lsec::bitsliced_variant() != 0 : true)
+                        : (kind == KWORDWISE || kind == KBITMATRIX || kind == KBITSLICEDW) ? lsec::bitsliced_variant() != 0
+                                                                                           : true)
     return 0;
   const void *cells = nullptr;
   int R = 0;

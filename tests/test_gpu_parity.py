@@ -102,6 +102,10 @@ def test_liberation_family_vs_reference(cuda, method, k, w):
     (L.LIBER8TION, 8, 8, 64, 24),
     (L.LIBER8TION, 3, 8, 16, 70),
     (L.BLAUM_ROTH, 16, 16, 32, 12),   # R*w = 32: 8 B lanes by the register cap
+    # Cauchy at w = 16 / 32: the coefficient bitmatrices, 4 B lanes
+    (L.CAUCHY_GOOD, 10, 16, 32, 20),
+    (L.CAUCHY_GOOD, 6, 32, 64, 9),
+    (L.CAUCHY_ORIG, 5, 32, 16, 11),
 ])
 def test_bitmatrix_network_vs_reference(cuda, method, k, w, P, nsuper):
     """Liberation-family codes on their compiled packet networks (ec_jit.cpp pktnet_source) once
@@ -112,14 +116,14 @@ def test_bitmatrix_network_vs_reference(cuda, method, k, w, P, nsuper):
 
     if not O.ref_available():
         pytest.skip("oracle/_ref not built")
-    m, n = 2, 3
+    m, n = (2 if method in (L.LIBERATION, L.BLAUM_ROTH, L.LIBER8TION) else 4), 3
     size = w * P * nsuper
     rng = np.random.default_rng(k * w + P)
     data = rng.integers(0, 256, (n, k, size), dtype=np.uint8)
     data[1] = 0xFF
     rp = O.RefPlan(method, k, m, w, P)
     want = np.stack([rp.encode(data[s]) for s in range(n)])
-    losses = ([0], [k - 1], [k], [k + 1], [0, k - 1], [1, k], [k, k + 1])
+    losses = ([0], [k - 1], [k], [k + 1], [0, k - 1], [1, k], [k, k + 1]) + (([0, 2, k + 1, k + 3], [1, 3, 4]) if m == 4 else ())
     with L.Plan.new(method, size, k, m, w, P, 8) as p:
         assert p.form_encoding_matrix() == 0 and p.form_decoding_matrix() == 0
         p.prepare_encode()
@@ -132,8 +136,8 @@ def test_bitmatrix_network_vs_reference(cuda, method, k, w, P, nsuper):
         assert np.array_equal(host[:, k:], want)
         for er in losses:
             p.prepare_decode(er)
-            if len(er) == 2 and er[0] < k:  # two outputs on a network (single erasures: k_bitmatrix)
-                assert p.jit(er) == 1, er
+            if len(er) >= 2 and er[0] < k and method in (L.LIBERATION, L.BLAUM_ROTH, L.LIBER8TION):
+                assert p.jit(er) == 1, er  # two outputs on a network (single erasures: k_bitmatrix)
             sh = host.copy()
             sh[:, er] = 0x33
             p.decode_stripes(sh, er)

@@ -79,8 +79,9 @@ def main():
         plan.prepare_decode([0])
         import time
         # heavy networks can take longer than prepare's 30 s wait; only codes that get one
-        # (ec_jit.cpp wants_xornet / wants_gfw_net: RS at w = 16 / 32, wide RS at w = 8)
-        has_net = meth == L.REED_SOL_VAN and (w in (16, 32) or m * k >= 96)
+        # (ec_jit.cpp wants_xornet / wants_gfw_net / wants_pktnet)
+        has_net = (w in (16, 32) and meth in (L.REED_SOL_VAN, L.CAUCHY_GOOD, L.CAUCHY_ORIG)) or \
+            (meth == L.REED_SOL_VAN and m * k >= 96) or meth in (L.LIBERATION, L.BLAUM_ROTH, L.LIBER8TION)
         t_end = time.time() + (90 if has_net else 0)
         while time.time() < t_end and not plan.jit():
             time.sleep(5)
