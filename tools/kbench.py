@@ -62,6 +62,7 @@ def main():
     ap.add_argument("--variants", default="0,0;1,0;0,2;0,4")
     ap.add_argument("--magic", action="store_true", help="also time fused encode+magic and standalone magic")
     ap.add_argument("--pad", type=int, default=0, help="bytes of padding after every shard (HBM channel spread)")
+    ap.add_argument("--lost", default="0", help="erasures of the timed decode, e.g. 0,1,k+1 as ids (default: D0)")
     ap.add_argument("--mix", action="store_true",
                     help="also time lsec_hbm_mix_dev over the same shards: the encode's traffic, XOR only")
     a = ap.parse_args()
@@ -74,9 +75,10 @@ def main():
         plan = L.Plan.for_chunk(meth, k, m, C, w)
         data = torch.randint(0, 256, (N, k, C + a.pad), dtype=torch.uint8, device=dev)[:, :, :C]
         par = torch.empty((N, m, C + a.pad), dtype=torch.uint8, device=dev)[:, :, :C]
-        out = torch.empty((N, 1, C), dtype=torch.uint8, device=dev)
+        lost = sorted({int(x) for x in a.lost.split(",")})
+        out = torch.empty((N, len(lost), C), dtype=torch.uint8, device=dev)
         plan.prepare_encode()  # wide codes: wait for the compiled XOR network (variant 0,0 uses it)
-        plan.prepare_decode([0])
+        plan.prepare_decode(lost)
         import time
         # heavy networks can take longer than prepare's 30 s wait; only codes that get one
         # (ec_jit.cpp wants_xornet / wants_gfw_net / wants_pktnet)
@@ -118,18 +120,20 @@ def main():
                     plan.encode_dev(data, par)
                 e1.record(stream)
                 for _ in range(a.reps):
-                    plan.decode_dev(data, par, [0], out=out)
+                    plan.decode_dev(data, par, lost, out=out)
                 e2.record(stream)
                 torch.cuda.synchronize()
                 res[v][0].append(e0.elapsed_time(e1) / a.reps)
                 res[v][1].append(e1.elapsed_time(e2) / a.reps)
                 assert torch.equal(par, ref_par), f"variant {v} changed parity"
-                assert torch.equal(out[:, 0], data[:, 0]), f"variant {v} decode mismatch"
+                for i, e in enumerate(lost):
+                    want = data[:, e] if e < k else ref_par[:, e - k]
+                    assert torch.equal(out[:, i], want), f"variant {v} decode mismatch (shard {e})"
         for v in variants:
             te = sorted(res[v][0])[len(res[v][0]) // 2]
             td = sorted(res[v][1])[len(res[v][1]) // 2]
             eb = (k + m) * C * N
-            db = (k + 1) * C * N
+            db = (k + len(lost)) * C * N
             print(f"{name:6s} N={N:5d} variant={v} jit={int(plan.jit()) if v == (0, 0) else 0}  encode {te:8.3f} ms {eb / te / 1e6:7.1f} GB/s "
                   f"({eb / te / 8e9:5.1%})   decode {td:8.3f} ms {db / td / 1e6:7.1f} GB/s ({db / td / 8e9:5.1%})",
                   flush=True)
