@@ -975,8 +975,28 @@ void bind_pkt_field(const void *image, const uint32_t *coef, int R, int K, int w
   bind_pkt(image, masks.data(), R, K, w, packet);
 }
 
+// hipRTC builds its compiler's global state at the first compile of the process, and the exit
+// destroys it in reverse order of construction: an exit handler registered before that state
+// exists runs after it is gone, too late to wait for a compile still using it.  So the first
+// bind compiles a trivial kernel here, on the calling thread, and only then registers the exit
+// drain, which then runs before that state is destroyed (tests/test_jit_queue.py).
+void warm_up_compiler() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    hiprtcProgram prog = nullptr;
+    if (hiprtcCreateProgram(&prog, "extern \"C\" __global__ void lsec_warm() {}\n", "lsec_warm.hip", 0, nullptr, nullptr) ==
+        HIPRTC_SUCCESS) {
+      const char *opts[] = {"--offload-arch=gfx950", "-O3"};
+      (void)hiprtcCompileProgram(prog, 2, opts);
+      hiprtcDestroyProgram(&prog);
+    }
+    atexit(drain_compiles);
+  });
+}
+
 void bind_key(const void *image, const std::vector<uint32_t> &key, const uint32_t *mat, size_t n, int R, int K, int w,
               int D, int S) {
+  warm_up_compiler();
   std::shared_ptr<Entry> e;
   bool start = false;
   {
@@ -997,8 +1017,7 @@ void bind_key(const void *image, const std::vector<uint32_t> &key, const uint32_
         ++g_workers;
         std::thread(compile_worker).detach();
       }
-      static std::once_flag once;
-      std::call_once(once, [] { atexit(drain_compiles); });
+
     } else {
       e = it->second;
     }
@@ -1116,3 +1135,33 @@ bool pkt_aligned(const ShardRef *in, int K, const ShardRef *out, int R, int w, i
 
 }  // namespace jit
 }  // namespace lsec
+
+extern "C" {
+
+// Test hook, not in include/ (no GPU; hipRTC compiles on the host): bind n distinct w = 16 RS-like
+// 4 x 10 matrices to stand-in image addresses (never dereferenced), wait up to wait_ms for the
+// first compile, unbind them all, and return how many compiles were ready by then.  A process
+// that returns right after leaves compiles queued and running for the exit drain
+// (tests/test_jit_queue.py).
+int lsec_test_jit_queue(int n, int wait_ms) {
+  if (n < 1 || n > 64 || wait_ms < 0) return -1;
+  static char stand_in[64];
+  std::vector<uint32_t> mat(40);
+  for (int i = 0; i < n; ++i) {
+    for (int c = 0; c < 40; ++c) mat[c] = static_cast<uint32_t>((c * 2654435761u + i * 40503u) & 0xFFFFu) | 1u;
+    lsec::jit::bind_entry(stand_in + i, mat.data(), 4, 10, 16);
+  }
+  (void)lsec::jit::wait(stand_in, wait_ms);
+  int ready = 0;
+  {
+    std::lock_guard<std::mutex> lk(lsec::jit::g_mu);
+    for (int i = 0; i < n; ++i) {
+      auto it = lsec::jit::g_by_image.find(stand_in + i);
+      if (it != lsec::jit::g_by_image.end() && it->second->state == lsec::jit::Entry::kReady) ++ready;
+    }
+  }
+  for (int i = 0; i < n; ++i) lsec::jit::unbind(stand_in + i);
+  return ready;
+}
+
+}  // extern "C"
