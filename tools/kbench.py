@@ -22,6 +22,9 @@ CONFIGS = {
     "cg63": (L.CAUCHY_GOOD, 6, 3, 1 << 20),
     "cg104": (L.CAUCHY_GOOD, 10, 4, 4 << 20),
     "rs206": (L.REED_SOL_VAN, 20, 6, 256 << 10),
+    "rs128": (L.REED_SOL_VAN, 12, 8, 512 << 10),
+    "rs166": (L.REED_SOL_VAN, 16, 6, 512 << 10),
+    "rs248": (L.REED_SOL_VAN, 24, 8, 256 << 10),
     "rs104c4": (L.REED_SOL_VAN, 10, 4, 4 << 20),
     "rs104c8": (L.REED_SOL_VAN, 10, 4, 8 << 20),
     "cg124c4": (L.CAUCHY_GOOD, 12, 4, 4 << 20),
