@@ -164,11 +164,18 @@ void share_pairs(std::vector<std::vector<Step>> &rows, int K, std::vector<std::p
 
 }  // namespace
 
+// dwords per lane: 16 B loads by default, 8 B for many-row networks over few inputs (R >= 8,
+// K <= 13, where 16 B would be two pieces per lane: RS(12+8) encode 0.67 -> 0.70,
+// profiles/r04_v15_xornet_ab.txt); LSEC_JIT_VARIANT bits 4-7 force 1 / 2 / 4
+int xornet_dwords(int R, int K) {
+  const int v = (jit_variant() >> 4) & 15;
+  if (v == 1 || v == 2 || v == 4) return v;
+  return R >= 8 && K * 8 <= 104 ? 2 : 4;
+}
+
 std::string xornet_source(const uint8_t *mat, int R, int K) {
   const int var = jit_variant();
-  // dwords per lane (16 B loads by default)
-  int D = (var >> 4) & 15;
-  if (D != 1 && D != 2 && D != 4) D = 4;
+  const int D = xornet_dwords(R, K);
   const int IT = D == 4 && K * 8 <= 104 ? 2 : 1;  // 16 B pieces per lane per shard (D = 4)
   const int lane_bytes = 4 * D * IT;
   const int tile = 256 * lane_bytes;
@@ -799,9 +806,8 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
   return s.str();
 }
 
-int xornet_tile(int K) {
-  int D = (jit_variant() >> 4) & 15;
-  if (D != 1 && D != 2 && D != 4) D = 4;
+int xornet_tile(int K, int R) {
+  const int D = xornet_dwords(R, K);
   const int IT = D == 4 && K * 8 <= 104 ? 2 : 1;
   return 256 * 4 * D * IT;
 }
@@ -1082,7 +1088,7 @@ hipError_t launch(hipFunction_t fn, int R, int K, const ShardRef *in, const Shar
   std::memcpy(args.data() + 16 + sizeof(ShardRef) * K, out, sizeof(ShardRef) * R);
   size_t bytes = args.size();
   void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes, HIP_LAUNCH_PARAM_END};
-  const int64_t tile = w == 8 ? xornet_tile(K) : gfw_tile(w, R);  // as xornet_source / gfw_source
+  const int64_t tile = w == 8 ? xornet_tile(K, R) : gfw_tile(w, R);  // as xornet_source / gfw_source
   const uint64_t ntiles = static_cast<uint64_t>((size + tile - 1) / tile) * static_cast<uint64_t>(nstripes);
   if (ntiles == 0) return hipSuccess;
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;

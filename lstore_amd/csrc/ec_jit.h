@@ -30,7 +30,7 @@ int gfw_tile(int w, int R);
 // whether the R-row network at w takes the wave-pair slice split (4 rows at w = 32; ec_jit.cpp)
 bool gfw_rowsplit(int w, int R);
 // bytes of a shard one 256-lane block of the network covers per tile
-int xornet_tile(int K);
+int xornet_tile(int K, int R);
 // LSEC_JIT_VARIANT (code shape knobs for A/B runs; 0 = default)
 int jit_variant();
 // Associate a device coefficient image with its matrix and start compiling that matrix's

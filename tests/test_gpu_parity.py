@@ -450,6 +450,7 @@ def test_wide_stripes_vs_oracle(cuda, method, k, m, size):
     (20, 6, 4096 * 3 + 24),  # ragged: the last lane's 16 B piece is 8 B
     (16, 6, 40968),          # R * K = 96: the smallest matrix served by a network
     (32, 8, 8192),           # the widest network (K = 32, R = 8)
+    (12, 8, 16384 + 40),     # R = 8 over K = 12: 8 B lanes, ragged last lane
 ])
 def test_xor_network_vs_oracle(cuda, k, m, size):
     """Wide RS codes run on their compiled XOR networks (ec_jit.cpp) once prepared: encode and
