@@ -102,11 +102,11 @@ bool wants_xornet(int R, int K) {
   return on && R >= 2 && R <= kMaxRows && K >= 2 && K <= kMaxCols && R * K >= 96;
 }
 
-// Code shape knobs (LSEC_JIT_VARIANT, read once; A/B runs): bit 0 = common-pair elimination,
-// bit 1 = doubling by shift-and-subtract instead of a packed 16-bit multiply, bits 4-7 = dwords
-// per lane (1, 2, 4; 0 = 4).  Measured on RS(20+6) (profiles/r02_v15_jit_ab.txt): all shapes
-// within 70.6-74.3 % of 8 TB/s, the default (4 dwords, packed multiply, no pair elimination)
-// best; pair elimination cuts VALU instructions 20 % but not time.  w = 16 / 32 networks: bits
+// Code shape knobs (LSEC_JIT_VARIANT, read once; A/B runs): bit 0 = uncapped common-pair
+// elimination, bit 3 = none (the default caps it by registers, xornet_source), bit 1 = doubling by
+// shift-and-subtract instead of a packed 16-bit multiply, bits 4-7 = dwords per lane (1, 2, 4;
+// 0 = xornet_dwords).  Round 2 measured the shapes on RS(20+6) encode within 70.6-74.3 % of 8 TB/s
+// (profiles/r02_v15_jit_ab.txt); round 4 capped pairs (r04_v15_xornet_ab.txt).  w = 16 / 32 networks: bits
 // 8-15 shared-pair cap, 16 unfenced loads, 17-18 inputs ahead, 21 serial XOR folds (gfw_source);
 // 19 turns the wave-pair split of 4-row w = 32 networks off, 20-23 shape it
 // (gfw_rowsplit_source; profiles/r04_v7_gfw_w32_ab.md, r04_v9_gfw_w32_split.txt).
@@ -129,8 +129,9 @@ struct Step {
 // Greedy common-pair elimination over all steps of all rows (Paar's heuristic): the pair of
 // symbols that occurs together in the most XOR sets becomes a new symbol while it occurs in at
 // least 3 (one 2-input XOR then saves a term in each of them).
-void share_pairs(std::vector<std::vector<Step>> &rows, int K, std::vector<std::pair<int, int>> &pairs) {
-  for (;;) {
+void share_pairs(std::vector<std::vector<Step>> &rows, int K, std::vector<std::pair<int, int>> &pairs,
+                 int max_pairs = 1 << 30) {
+  while (static_cast<int>(pairs.size()) < max_pairs) {
     std::map<std::pair<int, int>, int> count;
     for (auto &row : rows)
       for (auto &st : row) {
@@ -195,7 +196,12 @@ std::string xornet_source(const uint8_t *mat, int R, int K) {
     }
   }
   std::vector<std::pair<int, int>> pairs;
+  // common-pair elimination, capped so that the inputs and the pairs (D*IT registers each) stay
+  // within about 128 registers: RS(20+6) encode 0.70 -> 0.74 and its 6-loss decode 0.65 -> 0.73,
+  // RS(24+8) encode 0.60 -> 0.66, RS(12+8) 0.68 -> 0.72 (profiles/r04_v15_xornet_ab.txt; uncapped,
+  // the pairs cost occupancy).  LSEC_JIT_VARIANT bit 0: no cap; bit 3: no pairs (the round-3 form)
   if (var & 1) share_pairs(rows, K, pairs);
+  else if (!(var & 8)) share_pairs(rows, K, pairs, std::max(0, (128 - K * D * IT) / (D * IT)));
   auto sym = [&](int x) { return (x < K ? "e" : "p") + std::to_string(x < K ? x : x - K) + "[d]"; };
 
   std::ostringstream s;
