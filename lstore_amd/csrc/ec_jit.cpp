@@ -864,6 +864,29 @@ std::vector<uint32_t> key_of(const uint32_t *mat, int R, int K, int w) {
   return k;
 }
 
+// hipRTC for gfx950: the code object, or the reason in err
+void compile_source(const std::string &src, std::string &err, std::vector<char> &code) {
+  hiprtcProgram prog = nullptr;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "lsec_xornet.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    err = "hiprtcCreateProgram failed";
+    return;
+  }
+  const char *opts[] = {"--offload-arch=gfx950", "-O3"};
+  if (hiprtcCompileProgram(prog, 2, opts) != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &log[0]);
+    err = "hiprtc compile failed: " + log.substr(0, 400);
+  } else {
+    size_t n = 0;
+    hiprtcGetCodeSize(prog, &n);
+    code.resize(n);
+    hiprtcGetCode(prog, code.data());
+  }
+  hiprtcDestroyProgram(&prog);
+}
+
 void compile(std::shared_ptr<Entry> e) {
   const auto t0 = std::chrono::steady_clock::now();
   std::string src;
@@ -875,27 +898,9 @@ void compile(std::shared_ptr<Entry> e) {
   } else {
     src = gfw_source(e->mat.data(), e->R, e->K, e->w);
   }
-  hiprtcProgram prog = nullptr;
   std::string err;
   std::vector<char> code;
-  if (hiprtcCreateProgram(&prog, src.c_str(), "lsec_xornet.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
-    err = "hiprtcCreateProgram failed";
-  } else {
-    const char *opts[] = {"--offload-arch=gfx950", "-O3"};
-    if (hiprtcCompileProgram(prog, 2, opts) != HIPRTC_SUCCESS) {
-      size_t n = 0;
-      hiprtcGetProgramLogSize(prog, &n);
-      std::string log(n, '\0');
-      if (n) hiprtcGetProgramLog(prog, &log[0]);
-      err = "hiprtc compile failed: " + log.substr(0, 400);
-    } else {
-      size_t n = 0;
-      hiprtcGetCodeSize(prog, &n);
-      code.resize(n);
-      hiprtcGetCode(prog, code.data());
-    }
-    hiprtcDestroyProgram(&prog);
-  }
+  compile_source(src, err, code);
   static const bool trace = getenv("LSEC_TRACE") != nullptr;
   if (trace || !err.empty())
     fprintf(stderr, "[lsec jit] %dx%d w=%d xor network: %s (%.2f s)\n", e->R, e->K, e->w, err.empty() ? "compiled" : err.c_str(),
@@ -1155,6 +1160,59 @@ extern "C" {
 // first compile, unbind them all, and return how many compiles were ready by then.  A process
 // that returns right after leaves compiles queued and running for the exit drain
 // (tests/test_jit_queue.py).
+// Test hook, not in include/ (no GPU): generate and compile, synchronously with hipRTC, the
+// network of a pseudo-random matrix for each generator shape -- shape 0: w = 8 XOR network
+// (R x K bytes), 1: w = 16 / 32 bit-sliced network (one wave, or the wave-pair split from 4 rows
+// at w = 32 / 5 rows at w = 16), 2: packet network over bitmatrix masks (w <= 32), 3: packet
+// network over GF(2^w) coefficients.  Returns 0, or -1 with the compiler's reason.
+int lsec_test_jit_compile(int shape, int R, int K, int w, int packet, unsigned seed) {
+  if (R < 1 || R > 8 || K < 1 || K > 32 || shape < 0 || shape > 3) return lsec::set_error("lsec_test_jit_compile: bad arguments");
+  unsigned x = seed * 2654435761u + 12345u;
+  auto rnd = [&x] {
+    x = x * 1103515245u + 12345u;
+    return x >> 7;
+  };
+  std::string src;
+  if (shape == 0) {
+    std::vector<uint8_t> m(static_cast<size_t>(R) * K);
+    for (auto &v : m) v = static_cast<uint8_t>(rnd() | 1u);
+    src = lsec::jit::xornet_source(m.data(), R, K);
+  } else if (shape == 1) {
+    if (w != 16 && w != 32) return lsec::set_error("lsec_test_jit_compile: w %d", w);
+    std::vector<uint32_t> m(static_cast<size_t>(R) * K);
+    for (auto &v : m) v = (rnd() ^ (rnd() << 16)) & (w == 16 ? 0xFFFFu : 0xFFFFFFFFu);
+    src = lsec::jit::gfw_source(m.data(), R, K, w);
+  } else {
+    if (w < 2 || w > 32 || packet < 4) return lsec::set_error("lsec_test_jit_compile: w %d packet %d", w, packet);
+    std::vector<uint32_t> masks(static_cast<size_t>(R) * w * K);
+    if (shape == 2) {
+      for (auto &v : masks) v = rnd() & rnd() & (w == 32 ? 0xFFFFFFFFu : (1u << w) - 1u);
+    } else {
+      if (w != 16 && w != 32) return lsec::set_error("lsec_test_jit_compile: w %d", w);
+      std::vector<uint32_t> coef(static_cast<size_t>(R) * K);
+      for (auto &v : coef) v = (rnd() ^ (rnd() << 16)) & (w == 16 ? 0xFFFFu : 0xFFFFFFFFu);
+      for (int r = 0; r < R; ++r)
+        for (int j = 0; j < K; ++j) {
+          uint32_t cx = coef[r * K + j];
+          for (int b = 0; b < w && cx; ++b) {
+            for (int l = 0; l < w; ++l)
+              if ((cx >> l) & 1u) masks[(static_cast<size_t>(r) * w + l) * K + j] |= 1u << b;
+            cx = lsec::jit::gfw_times_x(cx, w);
+          }
+        }
+    }
+    int D = 0, S = 1;
+    lsec::jit::pkt_shape(R, w, packet, &D, &S);
+    if (D == 0) return lsec::set_error("lsec_test_jit_compile: packet %d", packet);
+    src = lsec::jit::pktnet_source(masks.data(), R, K, w, D, S);
+  }
+  std::string err;
+  std::vector<char> code;
+  lsec::jit::compile_source(src, err, code);
+  if (!err.empty()) return lsec::set_error("lsec_test_jit_compile: %s", err.c_str());
+  return code.empty() ? lsec::set_error("lsec_test_jit_compile: no code object") : 0;
+}
+
 int lsec_test_jit_queue(int n, int wait_ms) {
   if (n < 1 || n > 64 || wait_ms < 0) return -1;
   static char stand_in[64];
