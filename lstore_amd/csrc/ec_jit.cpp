@@ -305,6 +305,10 @@ namespace {
 
 // c * x in GF(2^w), Jerasure's polynomials (galois.c:65-98: 0210013, 020000007)
 uint32_t gfw_times_x(uint32_t c, int w) {
+  if (w == 8) {  // Jerasure's GF(2^8), x^8 = x^4+x^3+x^2+1 (0x11D)
+    c <<= 1;
+    return (c & 0x100u) ? (c ^ 0x11Du) & 0xFFu : c;
+  }
   if (w == 16) {
     c <<= 1;
     return (c & 0x10000u) ? (c ^ 0x1100Bu) & 0xFFFFu : c;
@@ -830,6 +834,7 @@ struct Entry {
   std::map<int, hipModule_t> modules;     // device -> module
   std::map<int, hipFunction_t> functions; // device -> kernel
   std::string err;
+  std::vector<uint32_t> key;  // its g_by_matrix key
 };
 
 // leaked on purpose: a compile still running when the process exits may touch them
@@ -922,6 +927,21 @@ void compile_worker() {
       if (g_exiting) return;
       e = g_queue.front();
       g_queue.pop_front();
+      // a network whose every image was unbound (its plans destroyed before the compile started)
+      // is dropped: a later bind of the same matrix queues it afresh
+      bool bound = false;
+      for (const auto &kv : g_by_image)
+        if (kv.second == e) {
+          bound = true;
+          break;
+        }
+      if (!bound) {
+        g_by_matrix.erase(e->key);
+        e->state = Entry::kFailed;
+        e->err = "dropped: no longer bound";
+        g_cv.notify_all();
+        continue;
+      }
       ++g_running;
     }
     compile(e);
@@ -978,11 +998,14 @@ void bind_pkt(const void *image, const uint32_t *masks, int R, int K, int w, int
 void bind_pkt_field(const void *image, const uint32_t *coef, int R, int K, int w, int packet) {
   // the bitmatrix of each GF(2^w) coefficient: output packet l takes input packet x where bit l
   // of c * x^x is set (Cauchy's packet layout, k_gfw_bitsliced)
-  if (!image || !wants_pktnet(R, K, w) || (w != 16 && w != 32)) return;
+  if (!image || !wants_pktnet(R, K, w) || (w != 8 && w != 16 && w != 32)) return;
+  // w = 8: Cauchy's bit-sliced GF(2^8) (k_gf8_bitsliced's layout): Cauchy-good(10+4) at 4 MiB
+  // 0.72 -> 0.74, (6+3) level (profiles/r04_v17_pktnet_cauchy8.txt); LSEC_JIT_VARIANT bit 27: off
+  if (w == 8 && ((jit_variant() >> 27) & 1)) return;
   std::vector<uint32_t> masks(static_cast<size_t>(R) * w * K, 0u);
   for (int r = 0; r < R; ++r)
     for (int j = 0; j < K; ++j) {
-      uint32_t cx = coef[r * K + j] & (w == 16 ? 0xFFFFu : 0xFFFFFFFFu);
+      uint32_t cx = coef[r * K + j] & (w == 8 ? 0xFFu : w == 16 ? 0xFFFFu : 0xFFFFFFFFu);
       for (int x = 0; x < w && cx; ++x) {
         for (int l = 0; l < w; ++l)
           if ((cx >> l) & 1u) masks[(static_cast<size_t>(r) * w + l) * K + j] |= 1u << x;
@@ -1027,6 +1050,7 @@ void bind_key(const void *image, const std::vector<uint32_t> &key, const uint32_
       e->w = w;
       e->D = D;
       e->S = S;
+      e->key = key;
       g_by_matrix.emplace(key, e);
       start = true;
       g_queue.push_back(e);
@@ -1055,6 +1079,12 @@ int wait(const void *image, int timeout_ms) {
   auto it = g_by_image.find(image);
   if (it == g_by_image.end()) return 0;
   std::shared_ptr<Entry> e = it->second;
+  // a network someone waits for compiles next
+  auto q = std::find(g_queue.begin(), g_queue.end(), e);
+  if (q != g_queue.end() && q != g_queue.begin()) {
+    g_queue.erase(q);
+    g_queue.push_front(e);
+  }
   g_cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return e->state != Entry::kCompiling; });
   return e->state == Entry::kReady ? 1 : 0;
 }

@@ -48,7 +48,7 @@ std::string pktnet_source(const uint32_t *masks, int R, int K, int w, int D, int
 // bind a bitmatrix image (ungrouped row masks, K <= 16) to its packet network; the lane width
 // follows the packet size
 void bind_pkt(const void *image, const uint32_t *masks, int R, int K, int w, int packet);
-// the same for an R x K GF(2^w) coefficient matrix in Cauchy's packet layout (w = 16 / 32)
+// the same for an R x K GF(2^w) coefficient matrix in Cauchy's packet layout (w = 8 / 16 / 32)
 void bind_pkt_field(const void *image, const uint32_t *coef, int R, int K, int w, int packet);
 // out[r] packets = the bitmatrix rows' XORs of the input packets, every stripe; the shard bases
 // and strides must be aligned to the lane width (pkt_aligned)

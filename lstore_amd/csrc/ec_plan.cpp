@@ -401,8 +401,12 @@ int encode_cells_locked(PlanExt *e, int dev, const void **out) {
   CoefCell *d = nullptr;
   if (upload_cells(h, &d)) return -1;
   e->impl->enc_cells[dev] = d;
-  if (kernel_kind(e->pub.method, e->pub.w) == KBYTEWISE)  // wide codes: an XOR network, compiled in the background
+  if (kernel_kind(e->pub.method, e->pub.w) == KBYTEWISE) {  // wide codes: an XOR network, compiled in the background
     lsec::jit::bind(d, e->impl->coding.data(), rows, k);
+  } else if (kernel_kind(e->pub.method, e->pub.w) == KBITSLICED) {  // Cauchy w = 8: a packet network (A/B knob)
+    std::vector<uint32_t> c32(e->impl->coding.begin(), e->impl->coding.end());
+    lsec::jit::bind_pkt_field(d, c32.data(), rows, k, 8, e->pub.packet_size);
+  }
   *out = d;
   return 0;
 }
@@ -528,8 +532,13 @@ int decode_entry_locked(PlanExt *e, const std::vector<int> &ids, int dev, Decode
     CoefCell *d = nullptr;
     if (upload_cells(h, &d)) return -1;
     dc = ent.dev_cells.emplace(dev, d).first;
-    if (!ent.xor_only && kernel_kind(e->pub.method, e->pub.w) == KBYTEWISE)
+    if (!ent.xor_only && kernel_kind(e->pub.method, e->pub.w) == KBYTEWISE) {
       lsec::jit::bind(d, ent.dp.rows.data(), static_cast<int>(ent.dp.erased.size()), e->pub.data_strips);
+    } else if (!ent.xor_only && kernel_kind(e->pub.method, e->pub.w) == KBITSLICED) {
+      std::vector<uint32_t> c32(ent.dp.rows.begin(), ent.dp.rows.end());
+      lsec::jit::bind_pkt_field(d, c32.data(), static_cast<int>(ent.dp.erased.size()), e->pub.data_strips, 8,
+                                e->pub.packet_size);
+    }
   }
   *out = &ent;
   *cells = dc->second;
@@ -594,7 +603,8 @@ int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in,
       size -= whole;
     }
   }
-  if ((kind == KBITMATRIX || kind == KBITSLICEDW) && lsec::bitsliced_variant() == 0 && lsec::jit::wants_pktnet(R, K, w) &&
+  if ((kind == KBITMATRIX || kind == KBITSLICEDW || kind == KBITSLICED) && lsec::bitsliced_variant() == 0 &&
+      lsec::jit::wants_pktnet(R, K, w) &&
       lsec::jit::pkt_aligned(in, K, out, R, w, packet))
     if (hipFunction_t fn = lsec::jit::ready(image, R, K)) {  // the bitmatrix's compiled packet network
       const hipError_t err = lsec::jit::launch_pkt(fn, R, K, in, out, nstripes, size, packet, w, st);
@@ -1061,8 +1071,9 @@ int lsec_plan_jit(lio_erasure_plan_t *plan, const int *erasures) {
   if (!e) return 0;
   const int kind = kernel_kind(e->pub.method, e->pub.w);
   if (kind == KBYTEWISE ? lsec::bytewise_variant() != 0
-                        : (kind == KWORDWISE || kind == KBITMATRIX || kind == KBITSLICEDW) ? lsec::bitsliced_variant() != 0
-                                                                                           : true)
+                        : (kind == KWORDWISE || kind == KBITMATRIX || kind == KBITSLICEDW || kind == KBITSLICED)
+                            ? lsec::bitsliced_variant() != 0
+                            : true)
     return 0;
   const void *cells = nullptr;
   int R = 0;

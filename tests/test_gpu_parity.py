@@ -102,8 +102,10 @@ def test_liberation_family_vs_reference(cuda, method, k, w):
     (L.LIBER8TION, 8, 8, 64, 24),
     (L.LIBER8TION, 3, 8, 16, 70),
     (L.BLAUM_ROTH, 16, 16, 32, 12),   # R*w = 32: 8 B lanes by the register cap
-    # Cauchy at w = 16 / 32: the coefficient bitmatrices, 4 B lanes
-    (L.CAUCHY_GOOD, 10, 16, 32, 20),
+    # Cauchy at w = 8 / 16 / 32: the coefficient bitmatrices
+    (L.CAUCHY_GOOD, 10, 8, 64, 30),   # w = 8, 8 B lanes
+    (L.CAUCHY_ORIG, 8, 8, 32, 17),
+    (L.CAUCHY_GOOD, 10, 16, 32, 20),  # 4 B lanes
     (L.CAUCHY_GOOD, 6, 32, 64, 9),
     (L.CAUCHY_ORIG, 5, 32, 16, 11),
 ])
