@@ -27,6 +27,10 @@ CONFIGS = {
     "rs248": (L.REED_SOL_VAN, 24, 8, 256 << 10),
     "rs104c4": (L.REED_SOL_VAN, 10, 4, 4 << 20),
     "rs104c8": (L.REED_SOL_VAN, 10, 4, 8 << 20),
+    "cg104s": (L.CAUCHY_GOOD, 10, 4, 256 << 10),
+    "cg104m": (L.CAUCHY_GOOD, 10, 4, 512 << 10),
+    "cg104l": (L.CAUCHY_GOOD, 10, 4, 2 << 20),
+    "cg164c8": (L.CAUCHY_GOOD, 16, 4, 8 << 20),
     "cg124c4": (L.CAUCHY_GOOD, 12, 4, 4 << 20),
     "cg124c8": (L.CAUCHY_GOOD, 12, 4, 8 << 20),
     "rs164": (L.REED_SOL_VAN, 16, 4, 1 << 20),
@@ -65,6 +69,7 @@ def main():
     ap.add_argument("--variants", default="0,0;1,0;0,2;0,4")
     ap.add_argument("--magic", action="store_true", help="also time fused encode+magic and standalone magic")
     ap.add_argument("--pad", type=int, default=0, help="bytes of padding after every shard (HBM channel spread)")
+    ap.add_argument("--no-wait", action="store_true", help="do not wait for a network (A/B runs with it off)")
     ap.add_argument("--lost", default="0", help="erasures of the timed decode, e.g. 0,1,k+1 as ids (default: D0)")
     ap.add_argument("--mix", action="store_true",
                     help="also time lsec_hbm_mix_dev over the same shards: the encode's traffic, XOR only")
@@ -87,7 +92,7 @@ def main():
         # (ec_jit.cpp wants_xornet / wants_gfw_net / wants_pktnet)
         has_net = (w in (16, 32) and meth == L.REED_SOL_VAN) or (meth in (L.CAUCHY_GOOD, L.CAUCHY_ORIG) and k <= 16) or \
             (meth == L.REED_SOL_VAN and m * k >= 96) or meth in (L.LIBERATION, L.BLAUM_ROTH, L.LIBER8TION)
-        t_end = time.time() + (90 if has_net else 0)
+        t_end = time.time() + (90 if has_net and not a.no_wait else 0)
         while time.time() < t_end and not plan.jit():
             time.sleep(5)
             print(f"{name}: waiting for the encode network", flush=True)
