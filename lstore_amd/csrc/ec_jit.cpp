@@ -92,7 +92,7 @@ bool wants_pktnet(int R, int K, int w) {
   // liberation-family bitmatrices (one mask word per bit-row and input) of modest width, two
   // outputs (encodes, double erasures): single-erasure decodes measured 0.72 on a network against
   // 0.76 on k_bitmatrix (profiles/r04_v12_pktnet.txt)
-  return jit_on() && w >= 2 && w <= 32 && R >= 2 && R <= kMaxRows && K >= 1 && K <= 16 && R * w <= 256;
+  return jit_on() && w >= 2 && w <= 32 && R >= 2 && R <= kMaxRows && K >= 1 && K <= kMaxCols && R * w <= 256;
 }
 
 bool wants_xornet(int R, int K) {

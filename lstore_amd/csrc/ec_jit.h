@@ -45,7 +45,7 @@ bool wants_pktnet(int R, int K, int w);
 // HIP source of the packet network for bitmatrix row masks [(r*w + l)*K + j] (w <= 32), D dwords
 // per lane (exposed for tests and tools)
 std::string pktnet_source(const uint32_t *masks, int R, int K, int w, int D, int S = 1);
-// bind a bitmatrix image (ungrouped row masks, K <= 16) to its packet network; the lane width
+// bind a bitmatrix image (ungrouped row masks, K <= 32) to its packet network; the lane width
 // follows the packet size
 void bind_pkt(const void *image, const uint32_t *masks, int R, int K, int w, int packet);
 // the same for an R x K GF(2^w) coefficient matrix in Cauchy's packet layout (w = 8 / 16 / 32)

@@ -105,6 +105,7 @@ def test_liberation_family_vs_reference(cuda, method, k, w):
     # Cauchy at w = 8 / 16 / 32: the coefficient bitmatrices
     (L.CAUCHY_GOOD, 10, 8, 64, 30),   # w = 8, 8 B lanes
     (L.CAUCHY_ORIG, 8, 8, 32, 17),
+    (L.CAUCHY_GOOD, 20, 8, 32, 9),    # 20 inputs, 6 outputs: 4 B lanes
     (L.CAUCHY_GOOD, 10, 16, 32, 20),  # 4 B lanes
     (L.CAUCHY_GOOD, 6, 32, 64, 9),
     (L.CAUCHY_ORIG, 5, 32, 16, 11),
@@ -118,14 +119,14 @@ def test_bitmatrix_network_vs_reference(cuda, method, k, w, P, nsuper):
 
     if not O.ref_available():
         pytest.skip("oracle/_ref not built")
-    m, n = (2 if method in (L.LIBERATION, L.BLAUM_ROTH, L.LIBER8TION) else 4), 3
+    m, n = (2 if method in (L.LIBERATION, L.BLAUM_ROTH, L.LIBER8TION) else 6 if k == 20 else 4), 3
     size = w * P * nsuper
     rng = np.random.default_rng(k * w + P)
     data = rng.integers(0, 256, (n, k, size), dtype=np.uint8)
     data[1] = 0xFF
     rp = O.RefPlan(method, k, m, w, P)
     want = np.stack([rp.encode(data[s]) for s in range(n)])
-    losses = ([0], [k - 1], [k], [k + 1], [0, k - 1], [1, k], [k, k + 1]) + (([0, 2, k + 1, k + 3], [1, 3, 4]) if m == 4 else ())
+    losses = ([0], [k - 1], [k], [k + 1], [0, k - 1], [1, k], [k, k + 1]) + (([0, 2, k + 1, k + 3], [1, 3, 4]) if m >= 4 else ())
     with L.Plan.new(method, size, k, m, w, P, 8) as p:
         assert p.form_encoding_matrix() == 0 and p.form_decoding_matrix() == 0
         p.prepare_encode()

@@ -90,7 +90,7 @@ def main():
         import time
         # heavy networks can take longer than prepare's 30 s wait; only codes that get one
         # (ec_jit.cpp wants_xornet / wants_gfw_net / wants_pktnet)
-        has_net = (w in (16, 32) and meth == L.REED_SOL_VAN) or (meth in (L.CAUCHY_GOOD, L.CAUCHY_ORIG) and k <= 16) or \
+        has_net = (w in (16, 32) and meth == L.REED_SOL_VAN) or (meth in (L.CAUCHY_GOOD, L.CAUCHY_ORIG) and k <= 32) or \
             (meth == L.REED_SOL_VAN and m * k >= 96) or meth in (L.LIBERATION, L.BLAUM_ROTH, L.LIBER8TION)
         t_end = time.time() + (90 if has_net and not a.no_wait else 0)
         while time.time() < t_end and not plan.jit():
