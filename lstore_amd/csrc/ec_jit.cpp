@@ -70,6 +70,21 @@ std::string xor_chain(std::vector<std::string> t) {
   return t[0];
 }
 
+// How a network reads its shard table (struct Args { ...; Ref in[K]; Ref out[R]; }): "a." for the
+// kernel argument, or -- from 24 shards -- "ap->", an opaque pointer to the kernarg segment
+// re-read in every tile, so that the table's 4 (K + R) SGPRs are not hoisted out of the tile loop
+// and spilled to VGPR lanes (RS(24+8): 65 SGPRs spilled, 2661 -> 2339 VALU ops a tile, encode
+// 0.65 -> 0.71, 8-loss decode 0.62 -> 0.69; RS(12+8) spills 7 and loses 3 % with it:
+// profiles/r04_v18_xornet_reload.txt).  LSEC_JIT_VARIANT bit 28 forces it on, bit 30 off
+std::string shard_table(std::ostringstream &s, int K, int R, const char *ind) {
+  const int var = jit_variant();
+  if (((var >> 30) & 1) || !(((var >> 28) & 1) || K + R >= 24)) return "a.";
+  s << ind << "const __attribute__((address_space(4))) Args *ap = (const __attribute__((address_space(4))) Args *)"
+            "__builtin_amdgcn_kernarg_segment_ptr();\n"
+    << ind << "asm volatile(\"\" : \"+s\"(ap));\n";
+  return "ap->";
+}
+
 }  // namespace
 
 bool jit_on() {
@@ -267,10 +282,11 @@ std::string xornet_source(const uint8_t *mat, int R, int K) {
        "  for (unsigned t = t0; t < nt; t += nb) {\n"
        "    const unsigned s = t / tps;\n"
     << "    const long long o0 = (long long)(t - s * tps) * " << tile << " + threadIdx.x * " << 4 * D << ";\n";
+  const std::string A = shard_table(s, K, R, "    ");
   const int DL = D * IT;  // dwords per lane per shard
   for (int j = 0; j < K; ++j) {
-    s << "    u32 e" << j << "[" << DL << "];\n    { const unsigned long long p = a.in[" << j << "].base + (unsigned long long)s * a.in["
-      << j << "].stride;\n";
+    s << "    u32 e" << j << "[" << DL << "];\n    { const unsigned long long p = " << A << "in[" << j
+      << "].base + (unsigned long long)s * " << A << "in[" << j << "].stride;\n";
     for (int it = 0; it < IT; ++it)
       s << "      ld" << D << "(e" << j << " + " << D * it << ", p, o0 + " << 256 * 4 * D * it << ", C);\n";
     s << "    }\n";
@@ -292,7 +308,8 @@ std::string xornet_source(const uint8_t *mat, int R, int K) {
       for (int x : st.terms) terms.push_back(sym(x));
       s << "        h[d] = " << xor_chain(terms) << ";\n      }\n";
     }
-    s << "      const unsigned long long q = a.out[" << r << "].base + (unsigned long long)s * a.out[" << r << "].stride;\n";
+    s << "      const unsigned long long q = " << A << "out[" << r << "].base + (unsigned long long)s * " << A << "out[" << r
+      << "].stride;\n";
     for (int it = 0; it < IT; ++it) s << "      st" << D << "(h + " << D * it << ", q, o0 + " << 256 * 4 * D * it << ", C);\n";
     s << "    }\n";
   }
@@ -527,10 +544,11 @@ std::string gfw_rowsplit_source(const uint32_t *mat, int R, int K, int W) {
        "  for (unsigned t = t0; t < nt; t += nb) {\n"
        "    const unsigned s = t / tps;\n"
     << "    const long long base = (long long)(t - s * tps) * " << tile << " + (pair * 64 + lane) * 16;\n";
+  const std::string A = shard_table(s, K, R, "    ");
   for (int r = 0; r < R; ++r) s << "    u32 h" << r << "[" << HW << "];\n";
   s << "    u32 e0[W], e1[W];\n";
   auto ptr = [&](int j) {
-    return "a.in[" + std::to_string(j) + "].base + (unsigned long long)s * a.in[" + std::to_string(j) + "].stride + base";
+    return A + "in[" + std::to_string(j) + "].base + (unsigned long long)s * " + A + "in[" + std::to_string(j) + "].stride + base";
   };
   // step u's own inputs into buffer b: used[2u] (role 0) and used[2u+1] (role 1)
   auto load = [&](int u, int b) {
@@ -609,7 +627,8 @@ std::string gfw_rowsplit_source(const uint32_t *mat, int R, int K, int W) {
           << "] = v.y; f[" << po + 2 << "] = v.z; f[" << po + 3 << "] = v.w; }\n";
         for (int d = 0; d < 4; ++d) s << "        f[" << mo + d << "] = h" << r << "[" << 4 * q + d << "];\n";
       }
-      s << "        tr(f);\n        st(f, a.out[" << r << "].base + (unsigned long long)s * a.out[" << r << "].stride + base);\n      }\n";
+      s << "        tr(f);\n        st(f, " << A << "out[" << r << "].base + (unsigned long long)s * " << A << "out[" << r
+        << "].stride + base);\n      }\n";
     }
   };
   s << "    if (role == 0) {\n";
@@ -680,6 +699,7 @@ std::string pktnet_source(const uint32_t *masks, int R, int K, int W, int D, int
     << "    const unsigned colb = min((ct - s * tps) * " << tile << " + threadIdx.x * " << 4 * D << ", cols - " << 4 * D << "u);\n"
        "    const unsigned sp = colb / P;\n"
     << "    const long long off = (long long)sp * " << W << " * P + (colb - sp * P);\n";
+  const std::string A = shard_table(s, K, R, "    ");
   const int per_g = (W + S - 1) / S;
   // accumulators and input buffers declared once, shared by the groups' blocks (each group's
   // packet l uses slot l - l0): the compiler then gives the blocks the same registers
@@ -708,7 +728,7 @@ std::string pktnet_source(const uint32_t *masks, int R, int K, int W, int D, int
     }
     auto load = [&](size_t u) {
       const int j = used[u];
-      s << "      { const unsigned long long p = a.in[" << j << "].base + (unsigned long long)s * a.in[" << j
+      s << "      { const unsigned long long p = " << A << "in[" << j << "].base + (unsigned long long)s * " << A << "in[" << j
         << "].stride + off;\n";
       for (int x = 0; x < W; ++x)
         if ((need[u] >> x) & 1u) s << "        ld(e" << u % 2 << "_" << x << ", p + " << x << "ull * P);\n";
@@ -744,7 +764,8 @@ std::string pktnet_source(const uint32_t *masks, int R, int K, int W, int D, int
       s << "      }\n      __builtin_amdgcn_sched_barrier(0);\n";
     }
     for (int r = 0; r < R; ++r) {
-      s << "      { const unsigned long long q = a.out[" << r << "].base + (unsigned long long)s * a.out[" << r << "].stride + off;\n";
+      s << "      { const unsigned long long q = " << A << "out[" << r << "].base + (unsigned long long)s * " << A << "out[" << r
+        << "].stride + off;\n";
       for (int l = l0; l < l1; ++l) {
         if (!live[static_cast<size_t>(r) * W + l]) s << "        for (int d = 0; d < D; ++d) h" << r << "_" << l - l0 << "[d] = 0u;\n";
         s << "        st(h" << r << "_" << l - l0 << ", q + " << l << "ull * P);\n";
@@ -780,6 +801,7 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
        "  for (unsigned t = t0; t < nt; t += nb) {\n"
        "    const unsigned s = t / tps;\n"
     << "    const long long base = (long long)(t - s * tps) * " << tile << " + threadIdx.x * 16;\n";
+  const std::string A = shard_table(s, K, R, "    ");
   std::vector<std::string> acc;
   std::vector<int> rows;
   for (int r = 0; r < R; ++r) {
@@ -795,7 +817,8 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
   const size_t nbuf = static_cast<size_t>(ahead) + 1;
   auto load = [&](size_t u) {
     const int j = used[u];
-    s << "    ld(e" << u % nbuf << ", a.in[" << j << "].base + (unsigned long long)s * a.in[" << j << "].stride + base);\n";
+    s << "    ld(e" << u % nbuf << ", " << A << "in[" << j << "].base + (unsigned long long)s * " << A << "in[" << j
+      << "].stride + base);\n";
   };
   for (size_t b = 0; b < nbuf; ++b) s << "    u32 e" << b << "[W];\n";
   for (size_t u = 0; u < used.size() && u < static_cast<size_t>(ahead); ++u) load(u);
@@ -809,7 +832,7 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
   for (int r = 0; r < R; ++r) {
     for (int b = 0; b < W; ++b)
       if (!live[r][b]) s << "    h" << r << "[" << b << "] = 0u;\n";
-    s << "    tr(h" << r << ");\n    st(h" << r << ", a.out[" << r << "].base + (unsigned long long)s * a.out[" << r
+    s << "    tr(h" << r << ");\n    st(h" << r << ", " << A << "out[" << r << "].base + (unsigned long long)s * " << A << "out[" << r
       << "].stride + base);\n";
   }
   s << "  }\n}\n";
