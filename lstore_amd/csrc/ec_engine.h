@@ -152,6 +152,8 @@ struct RouteTable {
   size_t own_dma_min_run;      // LSEC_OWN_DMA_MIN_RUN_KB = 1024: ... and its DMA runs average this
   bool server;                 // LSEC_SERVER = 1: route 1 on
   size_t srv_nt_min;           // LSEC_SRV_NT_MIN_KB (off): server calls copying this much in use streaming stores
+  bool srv_early_out;          // LSEC_SRV_EARLY_OUT = 1: a spinning server caller copies each part's
+                               // outputs out as soon as that part is done, while later parts are served
   // transports
   bool pin_in_place;           // LSEC_NO_HOST_REGISTER unset: pageable batches may be pinned in place for DMA
   size_t pin_min_bytes;        // LSEC_PIN_MIN_KB = 8192: ... when the batch has at least this many bytes
@@ -330,7 +332,14 @@ int usable_cpus();  // affinity mask, capped by the cgroup CPU quota
 // until every flags[i] reaches wants[i] (wrapping u32 sequences) or `slice` passes; true when
 // all have.  n <= kMaxWaitFlags parks on a futex when spinning does not pay.
 constexpr int kMaxWaitFlags = 16;
-bool flag_wait(const unsigned *const *flags, const unsigned *wants, int n, std::chrono::microseconds slice);
+// Called by a spinning wait each time flags[0, upto) have all been reached (in order), so the caller
+// can consume finished parts while the rest are served.  Not called while the waiter is parked.
+struct WaitProgress {
+  void (*fn)(void *ctx, int upto);
+  void *ctx;
+};
+bool flag_wait(const unsigned *const *flags, const unsigned *wants, int n, std::chrono::microseconds slice,
+               const WaitProgress *progress = nullptr);
 // flag reaches v, bounded: after 2 s the stream's status decides (false, *rc = -1 with a message)
 bool wait_flag(const unsigned *flag, unsigned v, hipStream_t st, int *rc);
 extern std::atomic<unsigned long long> g_st_parks, g_st_spin_hits, g_st_claim_misses, g_st_claim_spins, g_st_wakes,

@@ -44,6 +44,7 @@ const RouteTable &routes() {
     r.own_dma_min_run = static_cast<size_t>(std::max(0L, env("LSEC_OWN_DMA_MIN_RUN_KB", 1024))) << 10;
     r.server = env("LSEC_SERVER", 1) != 0;
     r.srv_nt_min = env("LSEC_SRV_NT_MIN_KB", -1) < 0 ? SIZE_MAX : static_cast<size_t>(env("LSEC_SRV_NT_MIN_KB", 0)) << 10;
+    r.srv_early_out = env("LSEC_SRV_EARLY_OUT", 1) != 0;
     r.pin_in_place = getenv("LSEC_NO_HOST_REGISTER") == nullptr;
     r.pin_min_bytes = static_cast<size_t>(std::max(0L, env("LSEC_PIN_MIN_KB", 8192))) << 10;
     r.pin_min_run = static_cast<size_t>(std::max(0L, env("LSEC_PIN_MIN_RUN_KB", 2560))) << 10;

@@ -79,14 +79,21 @@ class FlagWaits {
   // slices.  One wait covers all the parts of a call: the parts land on different server
   // workgroups and finish in any order (a wait per part could park and wake its thread once
   // per part under load).
-  bool wait(const unsigned *const *flags, const unsigned *wants, int n, std::chrono::microseconds slice) {
-    int from = 0;
-    if (reached_all(flags, wants, n, from)) return true;
+  bool wait(const unsigned *const *flags, const unsigned *wants, int n, std::chrono::microseconds slice,
+            const WaitProgress *pr = nullptr) {
+    int from = 0, told = 0;
+    // reached_all, telling the caller (pr) each time the reached prefix grows
+    const auto check = [&] {
+      const bool all = reached_all(flags, wants, n, from);
+      if (pr && from > told) pr->fn(pr->ctx, told = from);
+      return all;
+    };
+    if (check()) return true;
     Record *rec = n <= kMaxFlags ? my_record() : nullptr;
     if (!rec) {  // no record: spin, then yield, then nap
       const auto t0 = std::chrono::steady_clock::now();
       for (unsigned i = 0;; ++i) {
-        if (reached_all(flags, wants, n, from)) return true;
+        if (check()) return true;
         if (i < 500) {
           __builtin_ia32_pause();
           continue;
@@ -104,7 +111,7 @@ class FlagWaits {
     const int active = spinners_.fetch_add(1, std::memory_order_relaxed) + 1;
     if (short_waits && active <= spin_limit_) {
       for (unsigned i = 1;; ++i) {
-        if (reached_all(flags, wants, n, from)) {
+        if (check()) {
           spinners_.fetch_sub(1, std::memory_order_relaxed);
           note(t0);
           g_st_spin_hits.fetch_add(1, std::memory_order_relaxed);
@@ -302,8 +309,9 @@ bool wait_flag(const unsigned *flag, unsigned v, hipStream_t st, int *rc) {
   return true;
 }
 
-bool flag_wait(const unsigned *const *flags, const unsigned *wants, int n, std::chrono::microseconds slice) {
-  return FlagWaits::get().wait(flags, wants, n, slice);
+bool flag_wait(const unsigned *const *flags, const unsigned *wants, int n, std::chrono::microseconds slice,
+               const WaitProgress *progress) {
+  return FlagWaits::get().wait(flags, wants, n, slice, progress);
 }
 
 }  // namespace eng
