@@ -333,7 +333,7 @@ int usable_cpus();  // affinity mask, capped by the cgroup CPU quota
 // all have.  n <= kMaxWaitFlags parks on a futex when spinning does not pay.
 constexpr int kMaxWaitFlags = 16;
 // Called by a spinning wait each time flags[0, upto) have all been reached (in order), so the caller
-// can consume finished parts while the rest are served.  Not called while the waiter is parked.
+// can consume finished parts while the rest are served.  A parked waiter reports on waking.
 struct WaitProgress {
   void (*fn)(void *ctx, int upto);
   void *ctx;

@@ -146,7 +146,7 @@ class FlagWaits {
       futex_wait(&rec->word, 0, std::chrono::duration_cast<std::chrono::nanoseconds>(deadline - now));
     }
     rec->active.store(0, std::memory_order_release);
-    if (!reached_all(flags, wants, n, from)) {
+    if (!check()) {
       g_st_slices.fetch_add(1, std::memory_order_relaxed);
       return false;
     }
@@ -340,6 +340,7 @@ int lsec_selftest_waits(int threads, int iters) {
     pairs.back()->n = 1 + (t * 7) % 16;
   }
   std::atomic<int> bad{0};
+  std::atomic<unsigned long long> progress_calls{0};
   const unsigned long long parks0 = g_st_parks.load(), wakes0 = g_st_wakes.load();
   std::vector<std::thread> th;
   for (int t = 0; t < threads; ++t) {
@@ -361,11 +362,31 @@ int lsec_selftest_waits(int threads, int iters) {
       const unsigned *f[16];
       unsigned want[16];
       for (int i = 0; i < p.n; ++i) f[i] = &p.flags[i][0];
+      // the progress hook (WaitProgress): every prefix it reports must be reached, and grow
+      struct Seen {
+        const unsigned *const *f;
+        const unsigned *want;
+        int n, last;
+        std::atomic<int> *bad;
+        std::atomic<unsigned long long> *calls;
+      } seen{f, want, p.n, 0, &bad, &progress_calls};
+      const WaitProgress pr{[](void *ctx, int upto) {
+                              Seen &z = *static_cast<Seen *>(ctx);
+                              z.calls->fetch_add(1, std::memory_order_relaxed);
+                              bool ok = upto > z.last && upto <= z.n;
+                              for (int i = 0; ok && i < upto; ++i)
+                                ok = static_cast<int>(__atomic_load_n(z.f[i], __ATOMIC_ACQUIRE) - z.want[i]) >= 0;
+                              if (!ok) z.bad->store(3);
+                              z.last = upto;
+                            },
+                            &seen};
       for (int it = 0; it < iters && !bad.load(); ++it) {
         for (int i = 0; i < p.n; ++i) want[i] = static_cast<unsigned>(it + 1);
         p.ready.store(it, std::memory_order_release);
         const auto t0 = std::chrono::steady_clock::now();
-        while (!FlagWaits::get().wait(f, want, p.n, std::chrono::microseconds(500))) {
+        for (;;) {
+          seen.last = 0;  // each wait reports prefixes from the start
+          if (FlagWaits::get().wait(f, want, p.n, std::chrono::microseconds(500), (it & 1) ? &pr : nullptr)) break;
           if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
             bad.store(1);
             return;
@@ -382,9 +403,12 @@ int lsec_selftest_waits(int threads, int iters) {
   for (auto &x : th) x.join();
   if (bad.load() == 1) return fail("lsec_selftest_waits: a wait did not end within 2 s of its flags");
   if (bad.load() == 2) return fail("lsec_selftest_waits: a wait returned before all its flags were set");
+  if (bad.load() == 3) return fail("lsec_selftest_waits: a progress report named a flag not yet set, or shrank");
   // delays up to 300 us against a 30 us spin: long runs must have parked and been woken
   if (static_cast<long long>(threads) * iters >= 200 && (g_st_parks.load() == parks0 || g_st_wakes.load() == wakes0))
     return fail("lsec_selftest_waits: no waiter parked or was woken by a poller");
+  if (static_cast<long long>(threads) * iters >= 200 && progress_calls.load() == 0)
+    return fail("lsec_selftest_waits: no spinning wait reported progress");
   return 0;
 }
 
