@@ -81,6 +81,8 @@ def parse(argv=None):
     ap.add_argument("--json-out", default="", help="also write rank 0's JSON line to this file")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the in-run rocprofv3 PMC traffic passes (roofline.traffic from a committed profile)")
+    ap.add_argument("--share-gpus", action="store_true",
+                    help="allow more ranks than visible GPUs (a rehearsal: ranks share devices, and the line says so)")
     return ap.parse_args(argv)
 
 
@@ -187,6 +189,11 @@ def _run_killable(cmd, timeout, **kw):
         return None
 
 
+# a launcher's rank variables: the PMC child is a single-rank run of rank 0's geometry
+_DIST_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+             "GROUP_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+
 def pmc_traffic_live(a, N):
     """roofline.traffic measured for this run's configuration: two rocprofv3 --pmc passes
     (FETCH_SIZE, then WRITE_SIZE: they do not fit one pass, MI355X_MICROARCH.md) over a 1-step
@@ -213,7 +220,8 @@ def pmc_traffic_live(a, N):
             out = os.path.join(td, counter)
             cmd = ["rocprofv3", "--pmc", counter, "--kernel-trace", "--output-format", "csv", "-d", out, "-o", "pmc",
                    "--", sys.executable, os.path.abspath(__file__)] + args
-            rc = _run_killable(cmd, 240, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp", LSEC_BENCH_PMC_CHILD="1"),
+            env = {key: v for key, v in os.environ.items() if key not in _DIST_ENV and not key.startswith("TORCHELASTIC")}
+            rc = _run_killable(cmd, 240, cwd="/tmp", env=dict(env, TMPDIR="/tmp", LSEC_BENCH_PMC_CHILD="1"),
                                stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
             if rc != 0:
                 return None
@@ -301,7 +309,10 @@ class HipEngine:
         from lstore_amd import erasure as E
 
         self.torch, self.L, self.E, self.a = torch, L, E, a
-        torch.cuda.set_device(local % torch.cuda.device_count())
+        ndev = torch.cuda.device_count()
+        if local >= ndev and not a.share_gpus:
+            raise SystemExit(f"rank {rank}: local rank {local} but {ndev} visible GPU(s); --share-gpus for a rehearsal")
+        torch.cuda.set_device(local % ndev)
         self.dev = torch.device("cuda", torch.cuda.current_device())
         # control plane only (barrier, max, gather): gloo by default, RCCL opt-in
         self.backend = os.environ.get("LSEC_DIST_BACKEND", "gloo") if world > 1 else None
@@ -333,6 +344,24 @@ class HipEngine:
         # physical HBM pages an allocation gets moves these kernels by up to 8 % from one fresh
         # allocation to the next, the pad itself by about 1 % (profiles/r03_v4_alloc_probe.jsonl)
         self.room = 1024 if (world == 1 and not a.no_layout_ab) else 0
+
+    @staticmethod
+    def visible_devices():
+        """GPUs this process can see (torch.cuda.device_count does not initialise HIP on this image,
+        so the launcher may ask before it spawns the ranks)"""
+        import torch
+        return torch.cuda.device_count()
+
+    def device_identity(self):
+        """which physical GPU this rank runs on: index, PCI bus id and UUID"""
+        props = self.torch.cuda.get_device_properties(self.dev)
+        import ctypes
+        buf = ctypes.create_string_buffer(64)
+        hip = ctypes.CDLL("libamdhip64.so")
+        bus = buf.value.decode() if hip.hipDeviceGetPCIBusId(buf, 64, self.dev.index) == 0 else None
+        uuid = getattr(props, "uuid", None)
+        return {"index": self.dev.index, "pci_bus_id": bus, "uuid": str(uuid) if uuid is not None else None,
+                "name": props.name}
 
     def init_dist(self, dist):
         if self.backend == "nccl":
@@ -572,6 +601,23 @@ def run_rank(a, rank, world, local, engine_cls=HipEngine):
         # reduction and the gather of per-rank figures (RCCL by default)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         eng.init_dist(dist)
+    # which physical GPU every rank runs on, checked before any work: N ranks must be N devices
+    # unless the run says it is a rehearsal (--share-gpus)
+    ident = eng.device_identity() if hasattr(eng, "device_identity") else None
+    idents = [ident]
+    if world > 1:
+        idents = [None] * world
+        dist.all_gather_object(idents, ident)
+    dup = duplicate_devices(idents)
+    if dup and not a.share_gpus:
+        if rank == 0:
+            print(json.dumps({"error": f"ranks {dup} run on the same GPU; --share-gpus for a rehearsal",
+                              "devices": idents}), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        eng.close()
+        raise SystemExit(1)
     k, m, C, N = a.k, a.m, a.chunk, a.stripes
     first = rank * N  # global index of this rank's first stripe
     if a.total_stripes > 0:
@@ -610,7 +656,7 @@ def run_rank(a, rank, world, local, engine_cls=HipEngine):
     data_bytes = k * C * N
     enc_hbm = (k + m) * C * N
     dec_hbm = (k + 1) * C * N
-    mine = {"rank": rank, "stripes": N, "parity_ok": ok,
+    mine = {"rank": rank, "device": ident, "stripes": N, "parity_ok": ok,
             "encode_gibps": round(data_bytes / t_enc / 2**30, 2), "decode_gibps": round(data_bytes / t_dec / 2**30, 2),
             "encode_frac": round(enc_hbm / t_enc / HBM_PEAK, 4), "decode_frac": round(dec_hbm / t_dec / HBM_PEAK, 4),
             "avg_encode_launch_ms": round(t_enc * 1e3, 4), "avg_decode_launch_ms": round(t_dec * 1e3, 4)}
@@ -669,7 +715,10 @@ def run_rank(a, rank, world, local, engine_cls=HipEngine):
                                    f"{N} stripes/GPU, k*C={k * C} B user data per stripe",
                        "method": method, "k": k, "m": m, "chunk_bytes": C, "packet_size": eng.P,
                        "stripes_per_gpu": N, "lost_shard": a.lost, "shard_pad_bytes": a.pad,
-                       "parallelism": f"static stripe partition x{world}"},
+                       "parallelism": f"static stripe partition x{world}" + (
+                           f" (rehearsal: {world} ranks on {len({_dev_key(d) for d in idents})} GPU(s), --share-gpus)"
+                           if dup else "")},
+            "distinct_gpus": None if ident is None else len({_dev_key(d) for d in idents}),
             "encode_gibps": round(data_bytes / t_enc / 2**30, 2),
             "decode_gibps": round(data_bytes / t_dec / 2**30, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
@@ -698,6 +747,21 @@ def run_rank(a, rank, world, local, engine_cls=HipEngine):
     return out
 
 
+def _dev_key(d):
+    return None if d is None else (d.get("uuid") or d.get("pci_bus_id") or d.get("index"))
+
+
+def duplicate_devices(idents):
+    """rank lists of ranks that share one physical GPU ([] when every rank has its own, or when
+    the engine reports no identity)"""
+    by = {}
+    for r, d in enumerate(idents):
+        key = _dev_key(d)
+        if key is not None:
+            by.setdefault(key, []).append(r)
+    return [v for v in by.values() if len(v) > 1]
+
+
 # ----------------------------------------------------------------------------- launching
 def _free_port():
     with socket.socket() as s:
@@ -711,17 +775,35 @@ def _spawned(rank, a, world, port, engine_cls):
     run_rank(a, rank, world, rank, engine_cls)
 
 
+def preflight(a, engine_cls=HipEngine):
+    """The launch's arguments against the launcher and the visible devices: 0, or 2 after printing
+    the reason (before anything touches a GPU)."""
+    env_world = os.environ.get("WORLD_SIZE")
+    err = None
+    if a.gpus < 1:
+        err = f"--gpus {a.gpus} < 1"
+    elif env_world is not None and int(env_world) != a.gpus:
+        err = f"WORLD_SIZE={env_world} but --gpus {a.gpus}: launch one rank per GPU"
+    else:
+        visible = getattr(engine_cls, "visible_devices", None)
+        ndev = visible() if visible else None
+        if ndev is not None and a.gpus > ndev and not a.share_gpus:
+            err = (f"--gpus {a.gpus} but {ndev} GPU(s) visible: one rank per GPU "
+                   "(--share-gpus for a rehearsal that puts several ranks on one GPU)")
+    if err:
+        print(json.dumps({"error": err}), flush=True)
+        return 2
+    return 0
+
+
 def launch(a, engine_cls=HipEngine):
     """Run the benchmark on a.gpus ranks; returns the process exit code."""
     env_world = os.environ.get("WORLD_SIZE")
-    if a.gpus < 1:
-        print(json.dumps({"error": f"--gpus {a.gpus} < 1"}), flush=True)
-        return 2
+    rc = preflight(a, engine_cls)
+    if rc:
+        return rc
     if env_world is not None:
         world = int(env_world)
-        if world != a.gpus:
-            print(json.dumps({"error": f"WORLD_SIZE={world} but --gpus {a.gpus}: launch one rank per GPU"}), flush=True)
-            return 2
         run_rank(a, int(os.environ.get("RANK", "0")), world, int(os.environ.get("LOCAL_RANK", "0")), engine_cls)
         return 0
     if a.gpus == 1:
@@ -746,10 +828,20 @@ def launch(a, engine_cls=HipEngine):
 
 def main():
     a = parse()
-    if a.gpus == 1 and os.environ.get("WORLD_SIZE", "1") == "1" and not a.no_pmc:
-        # before this process touches the GPU: the counter passes run the same configuration as
-        # child processes under rocprofv3
-        a.traffic_live = pmc_traffic_live(a, a.total_stripes or a.stripes)
+    rc = preflight(a)
+    if rc:
+        sys.exit(rc)
+    if not a.no_pmc and os.environ.get("RANK", "0") == "0":
+        # before this process touches the GPU (before it spawns ranks, or, under a launcher, on
+        # rank 0 before it joins the others): the counter passes run rank 0's geometry as a
+        # single-rank child under rocprofv3, on rank 0's GPU
+        world = int(os.environ.get("WORLD_SIZE", a.gpus))
+        n0 = a.stripes
+        if a.total_stripes > 0:
+            from lstore_amd.partition import stripe_range
+            s0, s1 = stripe_range(a.total_stripes, world, 0)
+            n0 = s1 - s0
+        a.traffic_live = pmc_traffic_live(a, n0)
     sys.exit(launch(a))
 
 

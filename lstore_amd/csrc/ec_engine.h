@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "../../include/lstore_ec.h"
+#include "ec_hiperr.h"
 #include "ec_kernels.h"
 #include "gf8.h"
 

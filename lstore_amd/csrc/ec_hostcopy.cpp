@@ -147,7 +147,7 @@ class CopyPool {
   // the CPUs of a node, from any device placed on it
   static std::vector<int> node_cpus(int node) {
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) (void)hipGetLastError();
+    (void)quiet([&] { return hipGetDeviceCount(&n); });
     for (int d = 0; d < n; ++d)
       if (lsec::numa::of_device(d).node == node) return lsec::numa::of_device(d).cpus;
     return {};
@@ -347,8 +347,7 @@ static int d2h_pieces_direct(const std::vector<DevPiece> &pieces, hipStream_t st
       if (!(d >= abase && d < aend)) {
         hipDeviceptr_t b = nullptr;
         size_t sz = 0;
-        if (hipMemGetAddressRange(&b, &sz, d) != hipSuccess) {
-          (void)hipGetLastError();
+        if (quiet([&] { return hipMemGetAddressRange(&b, &sz, d); }) != hipSuccess) {
           b = d;  // unknown extent: no gap merging past this piece
           sz = p.bytes - done;
         }

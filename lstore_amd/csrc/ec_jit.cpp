@@ -29,11 +29,18 @@
 // of the coefficient, known at compile time, so every slice is a straight chain of 3-input XORs
 // (about w/4 per output slice per input) instead of the generic kernel's popcount(c) sweeps of
 // w XORs plus w-1 doublings.  gfw_source below.
+#include <dlfcn.h>
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
-#include <hip/hiprtc.h>
+#include <signal.h>
+#include <spawn.h>
+#include <sys/socket.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -43,11 +50,13 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <sstream>
 #include <string>
 #include <thread>
 #include <vector>
 
+#include "ec_hiperr.h"
 #include "ec_host.h"
 #include "ec_jit.h"
 
@@ -106,8 +115,11 @@ bool wants_gfw_net(int R, int K, int w) {
 bool wants_pktnet(int R, int K, int w) {
   // liberation-family bitmatrices (one mask word per bit-row and input) of modest width, two
   // outputs (encodes, double erasures): single-erasure decodes measured 0.72 on a network against
-  // 0.76 on k_bitmatrix (profiles/r04_v12_pktnet.txt)
-  return jit_on() && w >= 2 && w <= 32 && R >= 2 && R <= kMaxRows && K >= 1 && K <= kMaxCols && R * w <= 256;
+  // 0.76 on k_bitmatrix (profiles/r04_v12_pktnet.txt).  R * w <= 128: the measured shapes (4 rows
+  // at w = 32, Cauchy-good(10+4) 0.80, r04_v13_pktnet_cauchy.txt); 8 rows at w = 32 hold 256
+  // accumulator dwords per lane, and hipRTC took 320 s over one such network on the build host
+  // (6 s at 4 rows), so wider shapes stay on the generic kernels
+  return jit_on() && w >= 2 && w <= 32 && R >= 2 && R <= kMaxRows && K >= 1 && K <= kMaxCols && R * w <= 128;
 }
 
 bool wants_xornet(int R, int K) {
@@ -860,25 +872,37 @@ struct Entry {
   std::vector<uint32_t> key;  // its g_by_matrix key
 };
 
-// leaked on purpose: a compile still running when the process exits may touch them
+// leaked on purpose: a compile worker still waiting on its compiler when the process exits may
+// touch them
 std::mutex &g_mu = *new std::mutex();
 std::condition_variable &g_cv = *new std::condition_variable();
-// Compiles run on at most kWorkers threads fed from a queue.  hipRTC's compiler keeps global
-// state that the process's exit destroys, so a compile may not still run then: at exit no queued
-// compile starts and the running ones are waited for (a thread per network, as before, left a
-// dozen compiling at the end of a test run: heap corruption at exit).
+// Compiles run in child processes (lsec_jitc, ec_jitc.cpp), started by at most kWorkers threads
+// fed from a queue.  hipRTC never runs in this process: its compiler's global state, destroyed
+// by the process's exit under a compile still running, corrupted the heap in round 4, and the
+// wait for running compiles that fixed it held exit for as long as a compile takes (30 s for the
+// widest w = 32 networks on the build host).  At exit no queued compile starts and the running
+// compilers are killed; nothing is waited for (tests/test_jit_queue.py).
 constexpr int kWorkers = 2;
 auto &g_queue = *new std::deque<std::shared_ptr<struct Entry>>();
 int g_running = 0, g_workers = 0;
 bool g_exiting = false;
 // bumped whenever an image is bound or unbound: invalidates the threads' ready() caches
 std::atomic<uint64_t> g_gen{1};
+// the compiler processes running now (their own lock: the exit handler may run while a worker
+// holds g_mu)
+std::mutex &g_child_mu = *new std::mutex();
+auto &g_children = *new std::set<pid_t>();
+bool g_children_killed = false;
 
-void drain_compiles() {
-  std::unique_lock<std::mutex> lk(g_mu);
+void stop_compiles() {
+  {
+    std::lock_guard<std::mutex> lk(g_child_mu);
+    g_children_killed = true;
+    for (pid_t p : g_children) kill(p, SIGKILL);
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
   g_exiting = true;
   g_cv.notify_all();
-  g_cv.wait_for(lk, std::chrono::seconds(120), [] { return g_running == 0; });
 }
 auto &g_by_matrix = *new std::map<std::vector<uint32_t>, std::shared_ptr<Entry>>();  // key: R, K, w, matrix
 auto &g_by_image = *new std::map<const void *, std::shared_ptr<Entry>>();           // device image -> entry
@@ -892,27 +916,102 @@ std::vector<uint32_t> key_of(const uint32_t *mat, int R, int K, int w) {
   return k;
 }
 
-// hipRTC for gfx950: the code object, or the reason in err
+// lsec_jitc beside this library (LSEC_JITC overrides)
+const std::string &compiler_path() {
+  // leaked: a compile worker may still report a failure while the process exits
+  static const std::string &path = *new std::string([] {
+    if (const char *e = getenv("LSEC_JITC")) return std::string(e);
+    Dl_info info;
+    if (dladdr(reinterpret_cast<void *>(&compiler_path), &info) && info.dli_fname) {
+      std::string f(info.dli_fname);
+      const size_t slash = f.rfind('/');
+      return (slash == std::string::npos ? std::string(".") : f.substr(0, slash)) + "/lsec_jitc";
+    }
+    return std::string("lsec_jitc");
+  }());
+  return path;
+}
+
+// The exit handler is registered by the first compile (a handler that runs while no compile
+// exists has nothing to do).
+void register_exit_handler() {
+  static std::once_flag once;
+  std::call_once(once, [] { atexit(stop_compiles); });
+}
+
+// gfx950 code object of `src` from a compiler process (protocol in ec_jitc.cpp), or the reason in
+// err.  Sockets, not pipes: a write to a compiler that died must return EPIPE, not raise SIGPIPE
+// in the caller's process.
 void compile_source(const std::string &src, std::string &err, std::vector<char> &code) {
-  hiprtcProgram prog = nullptr;
-  if (hiprtcCreateProgram(&prog, src.c_str(), "lsec_xornet.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
-    err = "hiprtcCreateProgram failed";
+  register_exit_handler();
+  int in[2], out[2];
+  if (socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, in) != 0) {
+    err = "socketpair failed";
     return;
   }
-  const char *opts[] = {"--offload-arch=gfx950", "-O3"};
-  if (hiprtcCompileProgram(prog, 2, opts) != HIPRTC_SUCCESS) {
-    size_t n = 0;
-    hiprtcGetProgramLogSize(prog, &n);
-    std::string log(n, '\0');
-    if (n) hiprtcGetProgramLog(prog, &log[0]);
-    err = "hiprtc compile failed: " + log.substr(0, 400);
-  } else {
-    size_t n = 0;
-    hiprtcGetCodeSize(prog, &n);
-    code.resize(n);
-    hiprtcGetCode(prog, code.data());
+  if (socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, out) != 0) {
+    close(in[0]);
+    close(in[1]);
+    err = "socketpair failed";
+    return;
   }
-  hiprtcDestroyProgram(&prog);
+  posix_spawn_file_actions_t fa;
+  posix_spawn_file_actions_init(&fa);
+  posix_spawn_file_actions_adddup2(&fa, in[1], 0);
+  posix_spawn_file_actions_adddup2(&fa, out[1], 1);
+  posix_spawn_file_actions_addopen(&fa, 2, "/dev/null", O_WRONLY, 0);
+  const std::string ppid = std::to_string(getpid());
+  char *argv[] = {const_cast<char *>(compiler_path().c_str()), const_cast<char *>(ppid.c_str()), nullptr};
+  pid_t pid = -1;
+  int rc;
+  {
+    std::lock_guard<std::mutex> lk(g_child_mu);
+    rc = g_children_killed ? -1 : posix_spawn(&pid, argv[0], &fa, nullptr, argv, ::environ);
+    if (rc == 0) g_children.insert(pid);
+  }
+  posix_spawn_file_actions_destroy(&fa);
+  close(in[1]);
+  close(out[1]);
+  if (rc != 0) {
+    close(in[0]);
+    close(out[0]);
+    err = rc < 0 ? "exiting" : "cannot start the network compiler " + compiler_path() + ": " + strerror(rc);
+    return;
+  }
+  for (size_t o = 0; o < src.size();) {
+    const ssize_t w = send(in[0], src.data() + o, src.size() - o, MSG_NOSIGNAL);
+    if (w <= 0) break;  // the compiler died: its missing reply says so below
+    o += static_cast<size_t>(w);
+  }
+  close(in[0]);
+  std::vector<char> reply;
+  char buf[1 << 16];
+  for (;;) {
+    const ssize_t r = read(out[0], buf, sizeof(buf));
+    if (r <= 0) break;
+    reply.insert(reply.end(), buf, buf + r);
+  }
+  close(out[0]);
+  int status = 0;
+  while (waitpid(pid, &status, 0) < 0 && errno == EINTR) {
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_child_mu);
+    g_children.erase(pid);
+  }
+  uint64_t n = 0;
+  if (reply.size() >= 13)
+    for (int i = 0; i < 8; ++i) n |= static_cast<uint64_t>(static_cast<uint8_t>(reply[5 + i])) << (8 * i);
+  if (reply.size() < 13 || std::memcmp(reply.data(), "LSJC", 4) != 0 || reply.size() != 13 + n) {
+    std::lock_guard<std::mutex> lk(g_child_mu);
+    err = g_children_killed ? "exiting" : "the network compiler " + compiler_path() + " gave no answer";
+    return;
+  }
+  if (reply[4] != 0) {
+    err.assign(reply.begin() + 13, reply.end());
+    return;
+  }
+  code.assign(reply.begin() + 13, reply.end());
 }
 
 void compile(std::shared_ptr<Entry> e) {
@@ -930,7 +1029,7 @@ void compile(std::shared_ptr<Entry> e) {
   std::vector<char> code;
   compile_source(src, err, code);
   static const bool trace = getenv("LSEC_TRACE") != nullptr;
-  if (trace || !err.empty())
+  if ((trace || !err.empty()) && err != "exiting")
     fprintf(stderr, "[lsec jit] %dx%d w=%d xor network: %s (%.2f s)\n", e->R, e->K, e->w, err.empty() ? "compiled" : err.c_str(),
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
   std::lock_guard<std::mutex> lk(g_mu);
@@ -978,8 +1077,10 @@ hipFunction_t function_locked(Entry &e, int dev) {
   if (it != e.functions.end()) return it->second;
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr;
-  if (hipModuleLoadData(&mod, e.code.data()) != hipSuccess || hipModuleGetFunction(&fn, mod, "lsec_xornet") != hipSuccess) {
-    (void)hipGetLastError();
+  if (quiet([&] {
+        const hipError_t r = hipModuleLoadData(&mod, e.code.data());
+        return r != hipSuccess ? r : hipModuleGetFunction(&fn, mod, "lsec_xornet");
+      }) != hipSuccess) {
     e.state = Entry::kFailed;
     e.err = "module load failed";
     return nullptr;
@@ -1038,28 +1139,8 @@ void bind_pkt_field(const void *image, const uint32_t *coef, int R, int K, int w
   bind_pkt(image, masks.data(), R, K, w, packet);
 }
 
-// hipRTC builds its compiler's global state at the first compile of the process, and the exit
-// destroys it in reverse order of construction: an exit handler registered before that state
-// exists runs after it is gone, too late to wait for a compile still using it.  So the first
-// bind compiles a trivial kernel here, on the calling thread, and only then registers the exit
-// drain, which then runs before that state is destroyed (tests/test_jit_queue.py).
-void warm_up_compiler() {
-  static std::once_flag once;
-  std::call_once(once, [] {
-    hiprtcProgram prog = nullptr;
-    if (hiprtcCreateProgram(&prog, "extern \"C\" __global__ void lsec_warm() {}\n", "lsec_warm.hip", 0, nullptr, nullptr) ==
-        HIPRTC_SUCCESS) {
-      const char *opts[] = {"--offload-arch=gfx950", "-O3"};
-      (void)hiprtcCompileProgram(prog, 2, opts);
-      hiprtcDestroyProgram(&prog);
-    }
-    atexit(drain_compiles);
-  });
-}
-
 void bind_key(const void *image, const std::vector<uint32_t> &key, const uint32_t *mat, size_t n, int R, int K, int w,
               int D, int S) {
-  warm_up_compiler();
   std::shared_ptr<Entry> e;
   bool start = false;
   {
@@ -1208,12 +1289,7 @@ bool pkt_aligned(const ShardRef *in, int K, const ShardRef *out, int R, int w, i
 
 extern "C" {
 
-// Test hook, not in include/ (no GPU; hipRTC compiles on the host): bind n distinct w = 16 RS-like
-// 4 x 10 matrices to stand-in image addresses (never dereferenced), wait up to wait_ms for the
-// first compile, unbind them all, and return how many compiles were ready by then.  A process
-// that returns right after leaves compiles queued and running for the exit drain
-// (tests/test_jit_queue.py).
-// Test hook, not in include/ (no GPU): generate and compile, synchronously with hipRTC, the
+// Test hook, not in include/ (no GPU): generate and compile, synchronously (lsec_jitc), the
 // network of a pseudo-random matrix for each generator shape -- shape 0: w = 8 XOR network
 // (R x K bytes), 1: w = 16 / 32 bit-sliced network (one wave, or the wave-pair split from 4 rows
 // at w = 32 / 5 rows at w = 16), 2: packet network over bitmatrix masks (w <= 32), 3: packet
@@ -1266,13 +1342,23 @@ int lsec_test_jit_compile(int shape, int R, int K, int w, int packet, unsigned s
   return code.empty() ? lsec::set_error("lsec_test_jit_compile: no code object") : 0;
 }
 
-int lsec_test_jit_queue(int n, int wait_ms) {
-  if (n < 1 || n > 64 || wait_ms < 0) return -1;
+// Test hook, not in include/ (no GPU; the compiler runs on the host): bind n distinct pseudo-random
+// R x K GF(2^w) matrices (w = 16 / 32) to stand-in image addresses (never dereferenced), wait up to
+// wait_ms for the first compile, unbind them all, and return how many compiles were ready by then.
+// A process that returns right after leaves compiles queued and running at its exit
+// (tests/test_jit_queue.py).
+int lsec_test_jit_queue(int n, int wait_ms, int R, int K, int w, unsigned seed) {
+  if (n < 1 || n > 64 || wait_ms < 0 || R < 1 || R > 8 || K < 1 || K > 32 || (w != 16 && w != 32)) return -1;
   static char stand_in[64];
-  std::vector<uint32_t> mat(40);
+  std::vector<uint32_t> mat(static_cast<size_t>(R) * K);
+  unsigned x = seed * 2654435761u + 777u;
   for (int i = 0; i < n; ++i) {
-    for (int c = 0; c < 40; ++c) mat[c] = static_cast<uint32_t>((c * 2654435761u + i * 40503u) & 0xFFFFu) | 1u;
-    lsec::jit::bind_entry(stand_in + i, mat.data(), 4, 10, 16);
+    for (auto &c : mat) {
+      x = x * 1103515245u + 12345u;
+      c = ((x >> 5) ^ (x << 11)) & (w == 16 ? 0xFFFFu : 0xFFFFFFFFu);
+      c |= 2u;  // not an XOR-only row
+    }
+    lsec::jit::bind_entry(stand_in + i, mat.data(), R, K, w);
   }
   (void)lsec::jit::wait(stand_in, wait_ms);
   int ready = 0;

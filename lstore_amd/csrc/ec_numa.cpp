@@ -1,6 +1,8 @@
 // ec_numa.cpp -- device -> host NUMA node -> CPUs, and thread pinning (see ec_numa.h).
 #include "ec_numa.h"
 
+#include "ec_hiperr.h"
+
 #include <hip/hip_runtime.h>
 #include <pthread.h>
 #include <sched.h>
@@ -91,11 +93,9 @@ const Placement &of_device(int dev) {
     p.reset(new Placement());
     const char *off = getenv("LSEC_NUMA");
     char bus[64] = {0};
-    if (!(off && *off == '0') && hipDeviceGetPCIBusId(bus, sizeof(bus), dev) == hipSuccess) {
+    if (!(off && *off == '0') && quiet([&] { return hipDeviceGetPCIBusId(bus, sizeof(bus), dev); }) == hipSuccess) {
       const char *root = getenv("LSEC_SYSFS_ROOT");
       *p = for_bus(root ? root : "/sys", bus, g_allowed);
-    } else {
-      (void)hipGetLastError();
     }
   }
   return *p;

@@ -18,6 +18,23 @@
 #include "ec_engine.h"
 
 namespace lsec {
+
+hipError_t quiet(const std::function<hipError_t()> &f) {
+  if (hipPeekAtLastError() == hipSuccess) {
+    const hipError_t e = f();
+    if (e != hipSuccess) (void)hipGetLastError();  // the slot was clear: this error is the engine's own
+    return e;
+  }
+  // the caller's error is pending: run the call where its error cannot replace the caller's
+  hipError_t e = hipSuccess;
+  std::thread t([&] {
+    e = f();
+    if (e != hipSuccess) (void)hipGetLastError();
+  });
+  t.join();
+  return e;
+}
+
 namespace eng {
 
 std::atomic<unsigned long long> g_st_queries{0};  // runtime pointer queries (LSEC_STATS)
@@ -32,12 +49,11 @@ PtrInfo query_ptr(const void *ptr) {
   PtrInfo r;
   hipPointerAttribute_t attr;
   g_st_queries.fetch_add(1, std::memory_order_relaxed);
-  if (hipPointerGetAttributes(&attr, ptr) == hipSuccess) {
+  // (pageable host memory reports an error on some runtimes)
+  if (quiet([&] { return hipPointerGetAttributes(&attr, ptr); }) == hipSuccess) {
     r.ok = true;
     r.type = attr.type;
     r.dev = attr.devicePointer;
-  } else {
-    (void)hipGetLastError();  // pageable host memory reports an error on some runtimes
   }
   if (tl_memo_depth > 0 && tl_memo.size() < 64) tl_memo.push_back({ptr, r});  // small: scanned linearly
   return r;
@@ -75,9 +91,7 @@ bool inplace_overlaps_locked(uintptr_t lo, uintptr_t hi) {
 // (profiles/r04_alloc_kind_probe.jsonl).
 bool kernel_visible_allocation(const char *p) {
   unsigned flags = 0;
-  if (hipHostGetFlags(&flags, const_cast<char *>(p)) == hipSuccess) return true;
-  (void)hipGetLastError();
-  return false;
+  return quiet([&] { return hipHostGetFlags(&flags, const_cast<char *>(p)); }) == hipSuccess;
 }
 
 // p..p+len inside one page-locked allocation with a device alias?  (its device address in *dev;
@@ -94,10 +108,9 @@ bool pinned_chunk(const char *p, size_t len, std::vector<PinnedAlloc> &seen, uin
   if (!i.ok || i.type != hipMemoryTypeHost || !i.dev) return false;
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
-  if (hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(const_cast<char *>(p))) != hipSuccess) {
-    (void)hipGetLastError();
+  if (quiet([&] { return hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(const_cast<char *>(p))); }) !=
+      hipSuccess)
     return false;
-  }
   const uintptr_t lo = reinterpret_cast<uintptr_t>(base), hi = lo + size;
   if (u < lo || u + len > hi) return false;
   const intptr_t delta = reinterpret_cast<intptr_t>(i.dev) - static_cast<intptr_t>(u);
@@ -217,8 +230,8 @@ bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &
   for (const auto &r : regions) {
     char *lo = reinterpret_cast<char *>(reinterpret_cast<uintptr_t>(r.first) & ~(kPage - 1));
     char *hi = reinterpret_cast<char *>((reinterpret_cast<uintptr_t>(r.second) + kPage - 1) & ~(kPage - 1));
-    if (hipHostRegister(lo, static_cast<size_t>(hi - lo), hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
-      (void)hipGetLastError();
+    if (quiet([&] { return hipHostRegister(lo, static_cast<size_t>(hi - lo), hipHostRegisterPortable | hipHostRegisterMapped); }) !=
+        hipSuccess) {
       release();
       return false;
     }
@@ -229,8 +242,7 @@ bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &
 
 void InPlacePin::release() {
   for (char *b : held_)
-    if (hipHostUnregister(b) != hipSuccess) {
-      (void)hipGetLastError();
+    if (quiet([&] { return hipHostUnregister(b); }) != hipSuccess) {
       static std::atomic<bool> told{false};
       if (!told.exchange(true)) fprintf(stderr, "liblstore_ec: hipHostUnregister(%p) failed\n", static_cast<void *>(b));
     }

@@ -603,8 +603,7 @@ int lsec_set_host_devices(const int *devices, int n) {
   if (n > 0) {
     if (!devices) return fail("devices is NULL");
     int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess) {
-      (void)hipGetLastError();
+    if (lsec::quiet([&] { return hipGetDeviceCount(&count); }) != hipSuccess) {
       return fail("no HIP device");
     }
     for (int i = 0; i < n; ++i) {
@@ -622,8 +621,7 @@ int lsec_abi_version(void) { return LSEC_ABI_VERSION; }
 
 int lsec_device_count(void) {
   int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess) {
-    (void)hipGetLastError();
+  if (lsec::quiet([&] { return hipGetDeviceCount(&n); }) != hipSuccess) {
     return 0;
   }
   return n;
@@ -658,8 +656,7 @@ int lsec_hbm_mix_dev(const lsec_shard_t *shards, int k, int m, int nstripes, lon
 
 int lsec_device_numa(int dev, int *node, int *cpus, int max_cpus) {
   int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess) {
-    (void)hipGetLastError();
+  if (lsec::quiet([&] { return hipGetDeviceCount(&n); }) != hipSuccess) {
     n = 0;
   }
   if (dev < 0 || dev >= n) return fail("lsec_device_numa: no device %d", dev);

@@ -250,9 +250,8 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
           sl.pl = nullptr;
           sl.pl_cap = 0;
           const size_t cap = std::max(need, per * static_cast<size_t>(nb_max) * (nin + nout));
-          if (hipHostMalloc(reinterpret_cast<void **>(&sl.pl), cap * sizeof(lsec::CopyPiece), hipHostMallocDefault) !=
+          if (quiet([&] { return hipHostMalloc(reinterpret_cast<void **>(&sl.pl), cap * sizeof(lsec::CopyPiece), hipHostMallocDefault); }) !=
               hipSuccess) {
-            (void)hipGetLastError();
             sl.pl = nullptr;
             rc = fail("cannot allocate the copy-piece list");
             break;

@@ -365,8 +365,7 @@ class StripeServer {
     // the slot region: about 93 MiB per device, accounted as the device's server memory, apart
     // from the threads' slot budget (PinnedBudget)
     const size_t region = kSlotBytes * lsec::kSrvSlots;
-    if (hipHostMalloc(reinterpret_cast<void **>(&data_), region, hipHostMallocCoherent) != hipSuccess) {
-      (void)hipGetLastError();
+    if (quiet([&] { return hipHostMalloc(reinterpret_cast<void **>(&data_), region, hipHostMallocCoherent); }) != hipSuccess) {
       return fail("stripe server: cannot allocate its slots");
     }
     PinnedBudget::global().add_server(dev_, region);

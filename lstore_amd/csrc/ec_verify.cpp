@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "../../include/lstore_ec.h"
+#include "ec_hiperr.h"
 #include "ec_host.h"
 #include "ec_kernels.h"
 
@@ -539,12 +540,13 @@ bool all_zero(const char *p, size_t C) {
 void keep_pool() {
   int dev = 0;
   hipMemPool_t pool = nullptr;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess) {
-    (void)hipGetLastError();
+  if (lsec::quiet([&] {
+        const hipError_t r = hipGetDevice(&dev);
+        return r != hipSuccess ? r : hipDeviceGetDefaultMemPool(&pool, dev);
+      }) != hipSuccess)
     return;
-  }
   uint64_t keep = 2 * verify_budget();
-  if (hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep) != hipSuccess) (void)hipGetLastError();
+  (void)lsec::quiet([&] { return hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep); });
 }
 
 int stripes_per_batch(int n, int m, size_t C) {

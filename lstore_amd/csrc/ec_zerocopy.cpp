@@ -189,13 +189,11 @@ int run_zerocopy(PlanExt *e, char **ptrs, int nstripes, long long C, const std::
     // coherent: the kernel's reads and writes of the slot go straight over PCIe, none stays in an L2
     char *h = nullptr;
     void *d = nullptr;
-    if (hipHostMalloc(reinterpret_cast<void **>(&h), cap, hipHostMallocCoherent) != hipSuccess) {
-      (void)hipGetLastError();
+    if (quiet([&] { return hipHostMalloc(reinterpret_cast<void **>(&h), cap, hipHostMallocCoherent); }) != hipSuccess) {
       PinnedBudget::global().release_slot(dev, cap);
       return fail("zero-copy slot: cannot allocate %zu bytes of page-locked memory", cap);
     }
-    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
-      (void)hipGetLastError();
+    if (quiet([&] { return hipHostGetDevicePointer(&d, h, 0); }) != hipSuccess || !d) {
       (void)hipHostFree(h);
       PinnedBudget::global().release_slot(dev, cap);
       return fail("zero-copy slot: no device address");

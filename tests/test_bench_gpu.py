@@ -17,7 +17,7 @@ def test_bench_self_launches_two_ranks(cuda, tmp_path):
     env = dict(os.environ, LSEC_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "2", "--stripes", "64", "--steps", "3", "--warmup", "1",
-                        "--no-cpu", "--no-host-path", "--json-out", str(out)],
+                        "--no-cpu", "--no-host-path", "--share-gpus", "--json-out", str(out)],
                        cwd=ROOT, env=env, timeout=240, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     line = json.loads(out.read_text())
@@ -26,6 +26,21 @@ def test_bench_self_launches_two_ranks(cuda, tmp_path):
     assert all(p["parity_ok"] and p["stripes"] == 64 for p in line["per_rank"])
     assert line["parity_check"].startswith("bit-exact")
     assert line["value"] > 0 and line["roofline"]["frac"] > 0
+    # the one-GPU box: both ranks on one device, and the line says it is a rehearsal
+    assert line["distinct_gpus"] == 1 and "rehearsal" in line["config"]["parallelism"]
+    assert line["per_rank"][0]["device"]["pci_bus_id"] == line["per_rank"][1]["device"]["pci_bus_id"]
+    # the in-run PMC pass runs before the spawn at N > 1 too: traffic on the line
+    assert line["roofline"]["traffic"] and "measured in this run" in line["roofline"]["traffic_source"]
+
+
+@pytest.mark.gpu
+def test_bench_refuses_more_ranks_than_gpus(cuda):
+    """--gpus 2 on a one-GPU box without --share-gpus is refused before any rank starts"""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "-u", "bench.py", "--gpus", "2", "--stripes", "8", "--no-pmc"], cwd=ROOT, env=env,
+                       timeout=120, capture_output=True, text=True)
+    assert r.returncode == 2 and "GPU(s) visible" in r.stdout, r.stdout[-1000:] + r.stderr[-1000:]
 
 
 def test_bench_refuses_mismatched_world_size(tmp_path):

@@ -9,6 +9,7 @@ the union of the ranks' work is exactly the single-process result.
 """
 import json
 import os
+import shutil
 import time
 import zlib
 
@@ -41,11 +42,22 @@ class OracleEngine:
     def __init__(self, a, rank, world, local):
         import oracle as O
 
-        self.O, self.a, self.rank = O, a, rank
+        self.O, self.a, self.rank, self.local = O, a, rank, local
         self.method = O.REED_SOL_VAN if a.method == "reed_sol_van" else O.CAUCHY_GOOD
         self.P = O.generate_plan(a.k * a.chunk, self.method, a.k, a.m)["packet_size"]
         self.kernel = 1
         self.stripes = None
+
+    # a fake device set (the environment reaches spawned ranks): LSEC_TEST_FAKE_GPUS devices are
+    # visible; LSEC_TEST_FAKE_SAME=1 makes every rank report the same physical device
+    @staticmethod
+    def visible_devices():
+        return int(os.environ.get("LSEC_TEST_FAKE_GPUS", "64"))
+
+    def device_identity(self):
+        ndev = self.visible_devices()
+        idx = 0 if os.environ.get("LSEC_TEST_FAKE_SAME") == "1" else self.local % ndev
+        return {"index": idx, "pci_bus_id": "0000:%02x:00.0" % (0x10 + idx), "uuid": None, "name": "fake"}
 
     def init_dist(self, dist):
         dist.init_process_group("gloo")
@@ -195,6 +207,66 @@ def test_world_size_must_match_gpus(built, monkeypatch, capsys):
     monkeypatch.setenv("WORLD_SIZE", "2")
     assert bench.launch(_args("--gpus", "4"), OracleEngine) == 2
     assert "WORLD_SIZE=2" in capsys.readouterr().out
+
+
+def test_more_ranks_than_gpus_is_refused_unless_shared(built, tmp_path, monkeypatch, capsys):
+    """--gpus N beyond the visible devices is refused before any rank starts (VERDICT r04 item 3);
+    --share-gpus runs it as a rehearsal and the line says so."""
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setenv("LSEC_TEST_FAKE_GPUS", "1")
+    assert bench.launch(_args("--gpus", "2", "--stripes", "2"), OracleEngine) == 2
+    assert "1 GPU(s) visible" in capsys.readouterr().out
+    out = tmp_path / "line.json"
+    assert bench.launch(_args("--gpus", "2", "--stripes", "2", "--share-gpus", "--json-out", str(out)), OracleEngine) == 0
+    line = json.loads(out.read_text())
+    assert line["distinct_gpus"] == 1 and "rehearsal" in line["config"]["parallelism"]
+    assert [r["device"]["pci_bus_id"] for r in line["per_rank"]] == ["0000:10:00.0"] * 2
+
+
+def test_ranks_on_one_device_are_refused(built, monkeypatch, capfd):
+    """Two ranks that report the same physical GPU (bus id / UUID) stop before the timed region
+    unless --share-gpus is given."""
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setenv("LSEC_TEST_FAKE_SAME", "1")
+    assert bench.launch(_args("--gpus", "2", "--stripes", "2"), OracleEngine) == 1
+    assert "run on the same GPU" in capfd.readouterr().out
+
+
+def test_per_rank_devices_are_recorded(built, tmp_path, monkeypatch):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    out = tmp_path / "line.json"
+    assert bench.launch(_args("--gpus", "2", "--stripes", "2", "--json-out", str(out)), OracleEngine) == 0
+    line = json.loads(out.read_text())
+    assert line["distinct_gpus"] == 2 and "rehearsal" not in line["config"]["parallelism"]
+    assert [r["device"]["pci_bus_id"] for r in line["per_rank"]] == ["0000:10:00.0", "0000:11:00.0"]
+
+
+def test_duplicate_devices():
+    a, b = {"uuid": "u0", "pci_bus_id": "x"}, {"uuid": "u1", "pci_bus_id": "x"}
+    assert bench.duplicate_devices([a, b]) == []  # the UUID decides when present
+    assert bench.duplicate_devices([{"pci_bus_id": "x"}, {"pci_bus_id": "y"}, {"pci_bus_id": "x"}]) == [[0, 2]]
+    assert bench.duplicate_devices([None, None]) == []
+
+
+def test_pmc_child_runs_without_rank_variables(monkeypatch, tmp_path):
+    """The in-run PMC pass at N > 1 runs rank 0's geometry as a single-rank child: the launcher's
+    rank variables must not reach it (it would refuse WORLD_SIZE != --gpus)."""
+    seen = {}
+
+    def fake_run(cmd, timeout, **kw):
+        seen["cmd"], seen["env"] = cmd, kw["env"]
+        return 1  # as a failed pass: pmc_traffic_live gives up
+
+    monkeypatch.setattr(bench, "_run_killable", fake_run)
+    monkeypatch.setattr(shutil, "which", lambda x: "/bin/true")
+    for key, v in (("RANK", "0"), ("WORLD_SIZE", "8"), ("LOCAL_RANK", "0"), ("MASTER_PORT", "1234")):
+        monkeypatch.setenv(key, v)
+    for key in [k for k in os.environ if k.startswith("ROCPROF")]:
+        monkeypatch.delenv(key)
+    assert bench.pmc_traffic_live(_args("--gpus", "8", "--total-stripes", "100"), 13) is None
+    assert not {"RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"} & set(seen["env"])
+    i = seen["cmd"].index("--stripes")
+    assert seen["cmd"][i + 1] == "13" and "--total-stripes" not in seen["cmd"]
 
 
 def test_stripe_range_properties():

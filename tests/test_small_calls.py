@@ -208,19 +208,58 @@ import oracle as O
 hip = ctypes.CDLL("libamdhip64.so")
 junk = np.zeros(1 << 16, np.uint8)
 rng = np.random.default_rng(3)
-for C in (65536, 1 << 20):
-    p = L.Plan.for_chunk(L.CAUCHY_GOOD, 6, 3, C)
-    p.prepare_encode()
-    for _ in range(8):
-        d = rng.integers(0, 256, (9, C), dtype=np.uint8)
-        d[6:] = 0
-        # an unregister of memory that was never registered fails and leaves its error in this
-        # thread's HIP last-error slot, as the caller's own HIP calls can
-        assert hip.hipHostUnregister(ctypes.c_void_p(junk.ctypes.data)) != 0
-        p.encode_block([d[j] for j in range(9)])
-        assert np.array_equal(d[6:], O.encode(L.CAUCHY_GOOD, d[:6], 3, p.packet_size)), C
-        # ... and the caller's error is still there for the caller to read
-        assert hip.hipGetLastError() != 0, C
+
+
+def pageable(n):
+    return np.zeros(n, np.uint8), None
+
+
+def registered(n):
+    # the caller's own registration of its arena (DMA only inside the engine; telling it from
+    # hipHostMalloc memory takes a query that fails for registered ranges)
+    a = np.zeros(n + 4096, np.uint8)
+    off = (-a.ctypes.data) % 4096
+    a = a[off:off + n]
+    assert hip.hipHostRegister(ctypes.c_void_p(a.ctypes.data), ctypes.c_size_t(n), 0) == 0
+    return a, lambda: hip.hipHostUnregister(ctypes.c_void_p(a.ctypes.data))
+
+
+def hostmalloc(n):
+    p = ctypes.c_void_p()
+    assert hip.hipHostMalloc(ctypes.byref(p), ctypes.c_size_t(n), 0) == 0
+    a = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(p.value))
+    return a, lambda: hip.hipHostFree(p)
+
+
+for kind in (pageable, registered, hostmalloc):
+    for C in (65536, 1 << 20):
+        p = L.Plan.for_chunk(L.CAUCHY_GOOD, 6, 3, C)
+        p.prepare_encode()
+        p.prepare_decode([0])
+        arena, free = kind(9 * C)
+        d = arena.reshape(9, C)
+        for _ in range(4):
+            d[:6] = rng.integers(0, 256, (6, C), dtype=np.uint8)
+            d[6:] = 0
+            # an unregister of memory that was never registered fails and leaves its error in this
+            # thread's HIP last-error slot, as the caller's own HIP calls can
+            code = hip.hipHostUnregister(ctypes.c_void_p(junk.ctypes.data))
+            assert code != 0
+            p.encode_block([d[j] for j in range(9)])
+            assert np.array_equal(d[6:], O.encode(L.CAUCHY_GOOD, d[:6], 3, p.packet_size)), (kind.__name__, C)
+            # ... and exactly the caller's error is still there for the caller to read
+            got = hip.hipGetLastError()
+            assert got == code, (kind.__name__, C, "encode", got, code)
+            want = d[0].copy()
+            d[0] = 0
+            code = hip.hipHostUnregister(ctypes.c_void_p(junk.ctypes.data))
+            assert p.decode_block([d[j] for j in range(9)], [0]) == 0
+            assert np.array_equal(d[0], want), (kind.__name__, C)
+            got = hip.hipGetLastError()
+            assert got == code, (kind.__name__, C, "decode", got, code)
+        if free:
+            assert free() == 0
+        p.close()
 print("ok")
 """
 
