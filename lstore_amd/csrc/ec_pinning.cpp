@@ -106,12 +106,21 @@ bool pinned_chunk(const char *p, size_t len, std::vector<PinnedAlloc> &seen, uin
     }
   const PtrInfo i = query_ptr(p);
   if (!i.ok || i.type != hipMemoryTypeHost || !i.dev) return false;
-  hipDeviceptr_t base = nullptr;
+  // The extent of the page-locked range around p, as host addresses: the pointer attributes give
+  // it for both kinds; hipMemGetAddressRange gives the host range of hipHostMalloc memory only (for
+  // a hipHostRegister'ed range its base is not a host address, tools/probes/unregister_probe.py),
+  // so a caller-registered chunk never passed this check and was packed instead of DMA'd
+  void *start = nullptr;
   size_t size = 0;
-  if (quiet([&] { return hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(const_cast<char *>(p))); }) !=
-      hipSuccess)
+  if (quiet([&] {
+        const hipError_t r = hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR,
+                                                    reinterpret_cast<hipDeviceptr_t>(const_cast<char *>(p)));
+        return r != hipSuccess ? r
+                               : hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE,
+                                                        reinterpret_cast<hipDeviceptr_t>(const_cast<char *>(p)));
+      }) != hipSuccess)
     return false;
-  const uintptr_t lo = reinterpret_cast<uintptr_t>(base), hi = lo + size;
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(start), hi = lo + size;
   if (u < lo || u + len > hi) return false;
   const intptr_t delta = reinterpret_cast<intptr_t>(i.dev) - static_cast<intptr_t>(u);
   const bool kok = kernel_visible_allocation(p);
@@ -186,6 +195,17 @@ bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &
   size_t total = 0;
   for (const auto &r : regions) total += static_cast<size_t>(r.second - r.first);
   if (total < min_bytes) return false;  // packing a small batch is cheaper than the syscalls
+  // Never register pages someone has already page-locked: HIP keeps one registration per range,
+  // so registering a caller's registered arena again succeeds and our unregister at the end of
+  // the call then drops the CALLER's registration (its own hipHostUnregister later fails with
+  // hipErrorHostMemoryNotRegistered, and its kernels lose the mapping; round 5,
+  // tools/probes/unregister_probe.py).  Such memory is page-locked already: it packs (or DMAs in
+  // place when caller_pinned recognised it) instead.
+  for (const auto &r : regions)
+    for (const char *q : {static_cast<const char *>(r.first), static_cast<const char *>(r.second - 1)}) {
+      const PtrInfo i = query_ptr(q);
+      if (i.ok && i.type != hipMemoryTypeUnregistered) return false;
+    }
   // Each DMA from registered pageable memory has a fixed cost on top of the bytes, so pin
   // only when the copies the pinned path will issue (one per run of host-contiguous chunks,
   // stripe by stripe) average >= 2.5 MiB; smaller runs pack faster.  Round 1's 4 MiB had

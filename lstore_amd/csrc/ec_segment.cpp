@@ -41,24 +41,36 @@ class ParityPool {
     static ParityPool *pool = new ParityPool();  // leaked: lives until exit
     return *pool;
   }
+  // the smallest kept buffer that fits (a small call must not take a big one from the next big call)
   Buf acquire(size_t bytes) {
     std::lock_guard<std::mutex> lk(mu_);
+    size_t best = free_.size();
     for (size_t i = 0; i < free_.size(); ++i)
-      if (free_[i].cap >= bytes) {
-        Buf b = free_[i];
-        free_.erase(free_.begin() + static_cast<long>(i));
-        return b;
-      }
+      if (free_[i].cap >= bytes && (best == free_.size() || free_[i].cap < free_[best].cap)) best = i;
+    if (best < free_.size()) {
+      Buf b = free_[best];
+      kept_ -= b.cap;
+      free_.erase(free_.begin() + static_cast<long>(best));
+      return b;
+    }
     Buf b;
     b.p = static_cast<char *>(malloc(bytes));
     b.cap = b.p ? bytes : 0;
     return b;
   }
+  // keep at most kKeep buffers and kKeepBytes in total, the smallest first (one large segment
+  // write does not pin its parity heap for the life of the process)
   void release(Buf b) {
     std::lock_guard<std::mutex> lk(mu_);
+    if (b.cap > kKeepBytes) {
+      free(b.p);
+      return;
+    }
     free_.push_back(b);
-    std::sort(free_.begin(), free_.end(), [](const Buf &x, const Buf &y) { return x.cap > y.cap; });
-    while (free_.size() > kKeep) {
+    kept_ += b.cap;
+    std::sort(free_.begin(), free_.end(), [](const Buf &x, const Buf &y) { return x.cap < y.cap; });
+    while (free_.size() > kKeep || kept_ > kKeepBytes) {
+      kept_ -= free_.back().cap;
       free(free_.back().p);
       free_.pop_back();
     }
@@ -66,7 +78,9 @@ class ParityPool {
 
  private:
   static constexpr size_t kKeep = 4;
+  static constexpr size_t kKeepBytes = 256u << 20;
   std::mutex mu_;
+  size_t kept_ = 0;
   std::vector<Buf> free_;
 };
 

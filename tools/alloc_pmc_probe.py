@@ -27,12 +27,76 @@ import lstore_amd as L  # noqa: E402
 from alloc_probe import RawDev  # noqa: E402
 
 
+class VmmDev:
+    """A device buffer built with HIP's virtual memory API: physical chunks of `chunk` bytes
+    (hipMemCreate), mapped back to back (or in a shuffled order) into one reserved VA range, so
+    an allocation is made of many independently placed physical pieces instead of what one
+    hipMalloc returns.  Seen by torch through __cuda_array_interface__ (no copy)."""
+    hip = None
+
+    class Prop(ctypes.Structure):
+        _fields_ = [("type", ctypes.c_int), ("handle_type", ctypes.c_int), ("location", ctypes.c_int * 2),
+                    ("win32", ctypes.c_void_p), ("compression", ctypes.c_ubyte), ("rdma", ctypes.c_ubyte),
+                    ("usage", ctypes.c_ushort)]
+
+    class Access(ctypes.Structure):
+        _fields_ = [("location", ctypes.c_int * 2), ("flags", ctypes.c_int)]
+
+    def __init__(self, nbytes, chunk, shuffle_seed=None):
+        if VmmDev.hip is None:
+            VmmDev.hip = ctypes.CDLL("libamdhip64.so")
+        h = VmmDev.hip
+        prop = VmmDev.Prop(1, 0, (ctypes.c_int * 2)(1, torch.cuda.current_device()), None, 0, 0, 0)
+        gran = ctypes.c_size_t()
+        assert h.hipMemGetAllocationGranularity(ctypes.byref(gran), ctypes.byref(prop), 1) == 0
+        chunk = max(chunk, gran.value)
+        n = -(-nbytes // chunk)
+        self.size, self.chunk = n * chunk, chunk
+        p = ctypes.c_void_p()
+        assert h.hipMemAddressReserve(ctypes.byref(p), ctypes.c_size_t(self.size), ctypes.c_size_t(0), None,
+                                      ctypes.c_ulonglong(0)) == 0
+        self.ptr = p.value
+        self.handles = []
+        order = list(range(n))
+        if shuffle_seed is not None:
+            import random
+            random.Random(shuffle_seed).shuffle(order)
+        for i in range(n):
+            hd = ctypes.c_ulonglong()
+            rc = h.hipMemCreate(ctypes.byref(hd), ctypes.c_size_t(chunk), ctypes.byref(prop), ctypes.c_ulonglong(0))
+            if rc != 0:
+                raise MemoryError(f"hipMemCreate: error {rc}")
+            self.handles.append(hd)
+        for i, slot in enumerate(order):
+            assert h.hipMemMap(ctypes.c_void_p(self.ptr + slot * chunk), ctypes.c_size_t(chunk), ctypes.c_size_t(0),
+                               self.handles[i], ctypes.c_ulonglong(0)) == 0
+        acc = VmmDev.Access((ctypes.c_int * 2)(1, torch.cuda.current_device()), 3)
+        assert h.hipMemSetAccess(ctypes.c_void_p(self.ptr), ctypes.c_size_t(self.size), ctypes.byref(acc),
+                                 ctypes.c_size_t(1)) == 0
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (self.ptr, False),
+                                         "version": 3, "strides": None}
+
+    def tensor(self):
+        return torch.as_tensor(self, device="cuda")
+
+    def free(self):
+        if self.ptr:
+            torch.cuda.synchronize()
+            h = VmmDev.hip
+            h.hipMemUnmap(ctypes.c_void_p(self.ptr), ctypes.c_size_t(self.size))
+            for hd in self.handles:
+                h.hipMemRelease(hd)
+            h.hipMemAddressFree(ctypes.c_void_p(self.ptr), ctypes.c_size_t(self.size))
+            self.ptr = 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--trials", type=int, default=10)
     ap.add_argument("--stripes", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=6)
-    ap.add_argument("--alloc", default="torch", help="torch | hipmalloc | contig; a comma list alternates per trial")
+    ap.add_argument("--alloc", default="torch",
+                    help="torch | hipmalloc | contig | vmm:<chunk MiB>[:shuffle]; a comma list alternates per trial")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     k, m, C, N = 6, 3, 1 << 20, a.stripes
@@ -51,6 +115,17 @@ def main():
             dbuf = torch.randint(0, 256, (N * k * C,), dtype=torch.uint8, device=dev)
             pbuf = torch.empty((N * m * C,), dtype=torch.uint8, device=dev)
             rbuf = torch.empty((N * C,), dtype=torch.uint8, device=dev)
+        elif alloc.startswith("vmm"):
+            # vmm:<chunk MiB>[:shuffle]
+            parts = alloc.split(":")
+            chunk = int(parts[1]) << 20 if len(parts) > 1 else 2 << 20
+            seed = trial if len(parts) > 2 and parts[2] == "shuffle" else None
+            raws = [VmmDev(N * n * C, chunk, seed) for n in (k, m, 1)]
+            dbuf, pbuf, rbuf = (r.tensor() for r in raws)
+            g = torch.Generator(device=dev).manual_seed(trial)
+            for o in range(0, dbuf.numel(), 1 << 30):
+                seg = dbuf[o:o + (1 << 30)]
+                seg.copy_(torch.randint(0, 256, seg.shape, dtype=torch.uint8, device=dev, generator=g))
         else:
             raws = [RawDev(N * n * C, 4 if alloc == "contig" else -1) for n in (k, m, 1)]
             dbuf, pbuf, rbuf = (r.tensor() for r in raws)

@@ -16,6 +16,10 @@ PASS[dram2]="TCC_EA0_WRREQ_LEVEL_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_STALL_sum T
 PASS[chan]="$(for n in $(seq 0 15); do printf 'LSEC_RDREQ_CH%d ' $n; done)"
 PASS[wchan]="$(for n in $(seq 0 15); do printf 'LSEC_WRREQ_CH%d ' $n; done)"
 PASS[xcc]="$(for n in $(seq 0 7); do printf 'LSEC_RDREQ_XCC%d LSEC_RDLEV_XCC%d ' $n $n; done)"
+PASS[xcc2]="$(for n in $(seq 0 7); do printf 'LSEC_RDCS_XCC%d LSEC_RDGMI_XCC%d ' $n $n; done)"
+PASS[gmi]="TCC_EA0_RDREQ_GMI_32B_sum TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_RDREQ_IO_32B_sum TCC_EA0_RDREQ_GMI_CREDIT_STALL_sum"
+PASS[wgmi]="TCC_EA0_WRREQ_WRITE_GMI_32B_sum TCC_EA0_WRREQ_WRITE_DRAM_32B_sum TCC_EA0_WRREQ_GMI_CREDIT_STALL_sum TCC_EA0_WRREQ_LEVEL_sum"
+PASS[utcl]="TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum TCP_UTCL1_STALL_MULTI_MISS_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE"
 PASS[extra]="${LSEC_EXTRA_PMC:-}"
 TRIALS=${TRIALS:-8}
 PROBE="python $R/tools/alloc_pmc_probe.py --trials $TRIALS ${PROBE_ARGS:-}"

@@ -24,6 +24,27 @@ KM = [(4, 2), (6, 3), (8, 3), (8, 4), (10, 4), (12, 4), (16, 4), (20, 6)]
 CHUNKS = [256 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20, 8 << 20]
 
 
+def link_rates(torch, dev, nbytes=1 << 30, reps=5):
+    """This box's PCIe rate each way: one page-locked (hipHostMalloc) buffer <-> HBM, best of reps
+    (the ceiling every host-path point is measured against)"""
+    h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    best = {}
+    for name, dst, src in (("h2d", d, h), ("d2h", h, d)):
+        dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        t = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            dst.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+            t.append(time.perf_counter() - t0)
+        best[name + "_GBps"] = round(nbytes / min(t) / 1e9, 2)
+    del h, d
+    torch.cuda.empty_cache()
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--methods", default="reed_sol_van,cauchy_good")
@@ -49,6 +70,10 @@ def main():
     chunks = [int(x) for x in a.chunks.split(",")] if a.chunks else CHUNKS
     out = open(a.out, "a") if a.out else None
     stream = torch.cuda.current_stream()
+    link = link_rates(torch, dev)
+    print(json.dumps({"config": "c5", "rank": rank, "link": link}), flush=True)
+    if out:
+        out.write(json.dumps({"config": "c5", "rank": rank, "link": link}) + "\n")
     for mname in a.methods.split(","):
         meth = E.JE_METHOD_NAMES.index(mname)
         for k, m in km:
@@ -103,7 +128,14 @@ def main():
                        "enc_hbm_frac": round((k + m) * C * N / te / 8e12, 4),
                        "dec_hbm_frac": round((k + 1) * C * N / td / 8e12, 4),
                        "host_stripes": Nh, "host_enc_gibps": round(gib_h / the, 2),
-                       "host_dec_gibps": round(gib_h / thd, 2), "bit_exact": ok}
+                       "host_dec_gibps": round(gib_h / thd, 2),
+                       # the PCIe link's share each direction carries (encode: k*C in, m*C out per
+                       # stripe; decode: k*C survivors in, C out), against this box's measured rates
+                       "enc_h2d_link_frac": round(k * C * Nh / the / 1e9 / link["h2d_GBps"], 3),
+                       "enc_d2h_link_frac": round(m * C * Nh / the / 1e9 / link["d2h_GBps"], 3),
+                       "dec_h2d_link_frac": round(k * C * Nh / thd / 1e9 / link["h2d_GBps"], 3),
+                       "dec_d2h_link_frac": round(C * Nh / thd / 1e9 / link["d2h_GBps"], 3),
+                       "bit_exact": ok}
                 line = json.dumps(rec)
                 print(line, flush=True)
                 if out:
