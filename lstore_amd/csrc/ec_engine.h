@@ -166,6 +166,8 @@ struct RouteTable {
   int slot_pack_inline;        // 2
   // sizes
   size_t staging_bytes;        // LSEC_STAGING_MB = 128: route 4's page-locked budget per pipeline
+  size_t dev_staging_bytes;    // LSEC_DEV_STAGING_MB = 512: route 4's device slots when it DMAs in place
+                               // (no page-locked staging: only HBM, so whole stripes of wide codes fit)
   size_t slot_budget;          // LSEC_ZC_SLOTS_MB = 1024: route 2's slots per device (PinnedBudget)
   size_t dispatch_batch;       // 96 MiB packed per dispatcher batch
   int copy_threads;            // LSEC_COPY_THREADS = min(8, hardware threads): copy pool per NUMA node

@@ -87,9 +87,29 @@ struct ApplyArgs {
   int accumulate;         // 1: out[r] ^= the result (the second and later input groups of a wide stripe)
   unsigned long long *magic_acc;  // encode only (bytewise, bitsliced): fused stripe magic over the K inputs then the
                                   // R outputs (2 x u64 per stripe, zeroed), see MagicArgs
+  unsigned *tiles;        // work-sharing tile queue slot (tile_queue_slot), or null: each XCD its static eighth
   ShardRef in[kMaxK];
   ShardRef out[kMaxR];
 };
+
+// Work-sharing tiles.  The streaming kernels deal each XCD a contiguous eighth of the tiles
+// (xcd_remap), but the XCDs do not run at one rate: on the headline's memory shape the odd ones
+// take ~15 % longer per tile, every launch, so the even ones idle for the last 6-8 % of it
+// (tools/probes/xcd_balance.hip, profiles/r05_v2_xcd_balance.jsonl).  With a queue slot the grid
+// is persistent (the kernel's resident workgroups) and each workgroup takes tiles from its own
+// XCD's eighth through an atomic counter, then from the other eighths once its own is done, so
+// the XCDs finish within microseconds of each other.  A slot is kTileQueueWords counters on
+// lines of their own: one per eighth, then a done counter; the launch's last workgroup zeroes
+// them, and slots rotate over a ring per device, so a slot is reused only kTileQueueRing launches
+// later.  LSEC_TILES=static turns it off (A/B).
+constexpr int kTileQueueLine = 32;  // unsigned words per counter (a 128-B line each)
+constexpr int kTileQueueWords = 9 * kTileQueueLine;
+constexpr int kTileQueueRing = 4096;
+// a slot on the device of stream st; null: tile sharing off or unavailable (the static eighths serve)
+unsigned *tile_queue_slot(hipStream_t st);
+// the persistent grid of `kernel` on st's device (its resident workgroups of kBlock threads,
+// times the CUs), at most `grid`; 0 when the runtime cannot say
+int persistent_grid(const void *kernel, int grid, hipStream_t st);
 
 // Per-stripe adler32 "magic" of LStore's erasure segment (je_cksum_calc,
 // src/lio/segment/jerasure.c:169-182): zlib adler32 (RFC 1950) over the concatenation of all
@@ -190,6 +210,8 @@ void make_word_cell(uint32_t c, int w, uint32_t *out);
 
 // Variant selection knobs for experiments: 0 = default
 void set_kernel_variant(int bytewise_variant, int bitsliced_variant);
+void set_tile_sharing(bool on);  // lsec_set_tile_sharing
+bool tile_sharing();
 int bytewise_variant();  // != 0: a forced bytewise shape (also keeps wide codes off their XOR networks)
 int bitsliced_variant();  // != 0: a forced bit-sliced / wordwise variant (also keeps w = 16 / 32 RS off its XOR network)
 

@@ -1,8 +1,14 @@
 // ec_kernels.hip -- host-side launch policy for the gfx950 erasure kernels
 // (device code: ec_kernels_impl.h, instantiated per R in ec_kernels_inst.hip).
+#include <atomic>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
 #include <type_traits>
 
+#include "ec_hiperr.h"
 #include "ec_kernels_impl.h"
 
 namespace lsec {
@@ -15,6 +21,25 @@ int default_grid(uint64_t ntiles) {
   // One tile per block: on this streaming pattern a full grid beat every grid-stride
   // size from 2 to 16 blocks per CU by 5-7% (tools/kprobe.hip).
   return static_cast<int>(std::min<uint64_t>(std::max<uint64_t>(ntiles, 1), (1ull << 31) - 1));
+}
+
+constexpr int kQueueDevs = 64;
+std::once_flag g_queue_once[kQueueDevs];
+unsigned *g_queue[kQueueDevs];
+std::atomic<uint32_t> g_queue_next[kQueueDevs];
+int g_cus[kQueueDevs];
+
+std::atomic<int> g_tiles_shared{-1};  // -1: not read from LSEC_TILES yet
+
+bool tiles_shared() {
+  int v = g_tiles_shared.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char *e = getenv("LSEC_TILES");
+    int want = e && std::strcmp(e, "static") == 0 ? 0 : 1;
+    g_tiles_shared.compare_exchange_strong(v, want);
+    v = g_tiles_shared.load(std::memory_order_relaxed);
+  }
+  return v != 0;
 }
 
 template <typename F>
@@ -46,7 +71,81 @@ int bytewise_shape(int K, int R) {
   return K >= 16 ? 1 : 0;
 }
 
+// the device of stream st (the current device for the null stream), or -1
+int stream_device(hipStream_t st) {
+  int dev = -1;
+  if (quiet([&] { return st ? hipStreamGetDevice(st, &dev) : hipGetDevice(&dev); }) != hipSuccess) return -1;
+  return dev;
+}
+
 }  // namespace
+
+unsigned *tile_queue_slot(hipStream_t st) {
+  if (!tiles_shared()) return nullptr;
+  const int dev = stream_device(st);
+  if (dev < 0 || dev >= kQueueDevs) return nullptr;
+  std::call_once(g_queue_once[dev], [dev] {
+    const size_t bytes = sizeof(unsigned) * kTileQueueWords * kTileQueueRing;
+    void *p = nullptr;
+    int cus = 0, cur = -1;
+    // on st's device, which need not be the calling thread's current one
+    if (quiet([&] { return hipGetDevice(&cur); }) != hipSuccess) return;
+    if (cur != dev && quiet([&] { return hipSetDevice(dev); }) != hipSuccess) return;
+    struct Restore {
+      int cur, dev;
+      ~Restore() {
+        if (cur != dev) (void)quiet([&] { return hipSetDevice(cur); });
+      }
+    } restore{cur, dev};
+    if (quiet([&] { return hipMalloc(&p, bytes); }) != hipSuccess) return;
+    if (quiet([&] { return hipMemset(p, 0, bytes); }) != hipSuccess ||
+        quiet([&] { return hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev); }) != hipSuccess ||
+        cus <= 0) {
+      (void)hipFree(p);
+      return;
+    }
+    g_cus[dev] = cus;
+    g_queue[dev] = static_cast<unsigned *>(p);  // kept for the process's life
+  });
+  if (!g_queue[dev]) return nullptr;
+  const uint32_t i = g_queue_next[dev].fetch_add(1, std::memory_order_relaxed) % kTileQueueRing;
+  return g_queue[dev] + static_cast<size_t>(i) * kTileQueueWords;
+}
+
+int persistent_grid(const void *kernel, int grid, hipStream_t st) {
+  const int dev = stream_device(st);
+  if (dev < 0 || dev >= kQueueDevs || g_cus[dev] <= 0) return 0;
+  static std::mutex mu;
+  static std::map<const void *, int> per_cu;  // resident workgroups per CU, by kernel
+  int n = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = per_cu.find(kernel);
+    if (it != per_cu.end()) {
+      n = it->second;
+    } else {
+      if (quiet([&] { return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, kBlock, 0); }) != hipSuccess) n = 0;
+      per_cu[kernel] = n;
+    }
+  }
+  // LSEC_TILES_WGS overrides the workgroups per CU (A/B runs)
+  static const int force = [] {
+    const char *e = getenv("LSEC_TILES_WGS");
+    return e ? atoi(e) : 0;
+  }();
+  if (force > 0) n = force;
+  if (n <= 0) return 0;
+  // a multiple of 8: every XCD the same number of workgroups (blocks are dealt round-robin)
+  const int full = n * g_cus[dev];
+  const int pg = std::max(8, std::min(grid, full) & ~7);
+  static const bool trace = getenv("LSEC_TRACE") != nullptr;
+  if (trace) fprintf(stderr, "[lsec tiles] kernel %p: %d workgroups per CU x %d CUs -> grid %d (of %d tiles)\n", kernel, n, g_cus[dev], pg, grid);
+  return pg;
+}
+
+void set_tile_sharing(bool on) { g_tiles_shared.store(on ? 1 : 0, std::memory_order_relaxed); }
+
+bool tile_sharing() { return tiles_shared(); }
 
 void set_kernel_variant(int bw, int bs) {
   g_bw_variant = bw;
@@ -236,10 +335,10 @@ __global__ __launch_bounds__(kBlock) void k_gather(const GatherPiece *list, char
 // HBM probe: a plain streaming copy with the coding kernels' memory shape (one 8 KiB tile
 // per block, XCD-contiguous block order, 2 x 16 B non-temporal loads and stores per lane).
 // bench.py times it beside the encode as this box's practical read+write ceiling.
-__global__ __launch_bounds__(kBlock) void k_hbm_copy(uint64_t dst, uint64_t src, uint64_t n16) {
+__global__ __launch_bounds__(kBlock) void k_hbm_copy(uint64_t dst, uint64_t src, uint64_t n16, unsigned *tiles) {
   constexpr int kIt = 2;
-  const uint64_t ntiles = (n16 + kBlock * kIt - 1) / (kBlock * kIt);
-  for (uint64_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+  const uint32_t ntiles = static_cast<uint32_t>((n16 + kBlock * kIt - 1) / (kBlock * kIt));
+  for_tiles(ntiles, tiles, [&](uint64_t t) {
     const uint64_t i0 = t * kBlock * kIt + threadIdx.x;
     u32x4 v[kIt];
 #pragma unroll
@@ -252,7 +351,7 @@ __global__ __launch_bounds__(kBlock) void k_hbm_copy(uint64_t dst, uint64_t src,
       const uint64_t i = i0 + it * kBlock;
       if (i < n16) __builtin_nontemporal_store(v[it], gptr_w<u32x4>(dst + i * 16));
     }
-  }
+  });
 }
 
 // The encode's own traffic shape with no arithmetic (measurement probe): per stripe, the XOR of
@@ -264,7 +363,7 @@ __global__ __launch_bounds__(kBlock) void k_hbm_mix(ApplyArgs a) {
   const int64_t C = a.size;
   const uint32_t tps = static_cast<uint32_t>((C + kTile - 1) / kTile);
   const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
-  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+  for_tiles(ntiles, a.tiles, [&](uint32_t t) {
     const uint32_t s = t / tps;
     const int64_t off0 = static_cast<int64_t>(t - s * tps) * kTile + threadIdx.x * 16;
     u32x4 acc[kIt] = {0u, 0u};
@@ -297,7 +396,7 @@ __global__ __launch_bounds__(kBlock) void k_hbm_mix(ApplyArgs a) {
         }
       }
     }
-  }
+  });
 }
 
 // A small grid striding over the pieces, every lane holding its 4 x 16 B of a piece in flight
@@ -358,8 +457,15 @@ hipError_t launch_hbm_copy(void *dst, const void *src, uint64_t bytes, hipStream
   const uint64_t n16 = bytes / 16, ntiles = (n16 + kBlock * 2 - 1) / (kBlock * 2);
   if (ntiles == 0) return hipSuccess;
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
-  return launch_kernel(&k_hbm_copy, dim3(default_grid(ntiles)), dim3(kBlock), st, reinterpret_cast<uint64_t>(dst),
-                     reinterpret_cast<uint64_t>(src), n16);
+  int grid = default_grid(ntiles);
+  unsigned *q = tile_queue_slot(st);
+  if (q) {
+    const int pg = persistent_grid(reinterpret_cast<const void *>(&k_hbm_copy), grid, st);
+    if (pg > 0) grid = pg;
+    else q = nullptr;
+  }
+  return launch_kernel(&k_hbm_copy, dim3(grid), dim3(kBlock), st, reinterpret_cast<uint64_t>(dst),
+                     reinterpret_cast<uint64_t>(src), n16, q);
 }
 
 hipError_t launch_hbm_mix(const ApplyArgs &a, hipStream_t st) {
@@ -368,7 +474,7 @@ hipError_t launch_hbm_mix(const ApplyArgs &a, hipStream_t st) {
   const uint64_t tile = kBlock * 16 * 2;
   const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
-  return launch_kernel(&k_hbm_mix, dim3(default_grid(ntiles)), dim3(kBlock), st, a);
+  return launch_tiled(&k_hbm_mix, default_grid(ntiles), st, a);
 }
 
 hipError_t launch_gather(const GatherPiece *list, int n, char *dst, hipStream_t st) {

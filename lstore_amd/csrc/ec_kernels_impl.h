@@ -100,6 +100,68 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
   return xcd * per + min(xcd, rem) + (b >> 3);
 }
 
+// Every tile t < ntiles to body(t) exactly once, body's t uniform over the workgroup.  q null:
+// the grid strides over the tiles from its XCD-contiguous start (one tile per block when the grid
+// is the tile count).  q a tile queue slot (ec_kernels.h, "Work-sharing tiles"): the grid is
+// persistent; a workgroup takes G consecutive tiles at a time (a grab) from its own XCD's eighth
+// of the grabs, then from the other eighths'.  Thread 0 issues the atomic for the next grab before
+// the current grab's tiles and reads its result after them, so the counter's round trip hides
+// behind the tiles' loads; it posts the index in one of two LDS words (never one a wave has yet to
+// read: that wave has not passed the barrier after its read), and readfirstlane keeps the loop
+// exit uniform.
+template <int G = 1, typename Body>
+__device__ __forceinline__ void for_tiles(uint32_t ntiles, unsigned *q, Body &&body) {
+  if (q == nullptr) {
+    for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) body(t);
+    return;
+  }
+  __shared__ uint32_t next[2];
+  const uint32_t units = (ntiles + G - 1) / G, per = (units + 7) >> 3, xcd = blockIdx.x & 7;
+  uint32_t k = 0, pend = 0, it = 0;  // thread 0: eighths done, the counter value in flight
+  const auto take = [&]() -> uint32_t {  // thread 0: the grab `pend` names, or `units` when all are gone
+    for (;;) {
+      const uint32_t e = (xcd + k) & 7, u = e * per + pend;
+      if (pend < per && u < units) return u;
+      if (++k == 8) return units;
+      pend = atomicAdd(q + kTileQueueLine * ((xcd + k) & 7), 1u);
+    }
+  };
+  if (threadIdx.x == 0) {
+    pend = atomicAdd(q + kTileQueueLine * xcd, 1u);
+    next[0] = take();
+  }
+  __syncthreads();
+  uint32_t u = __builtin_amdgcn_readfirstlane(next[0]);
+  while (u < units) {
+    if (threadIdx.x == 0) pend = atomicAdd(q + kTileQueueLine * ((xcd + k) & 7), 1u);  // the next grab
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+      if (G == 1 || u * G + g < ntiles) body(u * G + g);
+    ++it;
+    if (threadIdx.x == 0) next[it & 1] = take();
+    __syncthreads();
+    u = __builtin_amdgcn_readfirstlane(next[it & 1]);
+  }
+  // the launch's last workgroup leaves the slot zeroed for its next use (kTileQueueRing launches on)
+  if (threadIdx.x == 0 && atomicAdd(q + kTileQueueLine * 8, 1u) == gridDim.x - 1)
+    for (int e = 0; e <= 8; ++e) atomicExch(q + kTileQueueLine * e, 0u);
+}
+
+// A tile-loop kernel over ApplyArgs, launched with a work-sharing tile queue slot and its
+// persistent grid when tile sharing is on (ec_kernels.h), else on `grid` blocks over static eighths.
+template <typename Kern>
+hipError_t launch_tiled(Kern *k, int grid, hipStream_t st, ApplyArgs a) {
+  a.tiles = tile_queue_slot(st);
+  if (a.tiles) {
+    const int pg = persistent_grid(reinterpret_cast<const void *>(k), grid, st);
+    if (pg > 0)
+      grid = pg;
+    else
+      a.tiles = nullptr;
+  }
+  return launch_kernel(k, dim3(grid), dim3(kBlock), st, a);
+}
+
 // ------------------------------------------------------------------ adler32 partial sums
 constexpr uint32_t kAdlerMod = 65521;
 
@@ -324,7 +386,8 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
   const uint32_t ntiles = tiles_per_stripe * static_cast<uint32_t>(a.nstripes);
   ConstCell *cells = const_cells(a.cells);
 
-  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+  // grabs of about 8 KiB per shard (the single-erasure decode's 2 KiB tiles go 4 at a time)
+  for_tiles<(kTile >= 8192 ? 1 : 8192 / kTile)>(ntiles, a.tiles, [&](uint32_t t) {
     const uint32_t s = t / tiles_per_stripe;
     const int64_t off0 = static_cast<int64_t>(t - s * tiles_per_stripe) * kTile + threadIdx.x * kLane;
     const bool full = (static_cast<int64_t>(t - s * tiles_per_stripe) + 1) * kTile <= C;  // wave-uniform
@@ -429,7 +492,7 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
       bw_magic_out<R, IT, VW>(ml, K, acc);
       ml_commit(ml, a.magic_acc, s, K + R, static_cast<uint64_t>(a.size), static_cast<uint64_t>(off0), kStep, red);
     }
-  }
+  });
 }
 
 // The XOR-row flag (CoefCell::pad bit 0 of the launch's first cell) picks one of two whole
@@ -463,13 +526,13 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
   const uint32_t ntiles = tiles_per_stripe * static_cast<uint32_t>(a.nstripes);
   ConstCell *cells = const_cells(a.cells);
 
-  for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) {
+  for_tiles(ntiles, a.tiles, [&](uint32_t t) {
     const uint32_t s = t / tiles_per_stripe;
     const uint32_t colb = (t - s * tiles_per_stripe) * kTile + threadIdx.x * (4 * DW);
     // lanes past the end occur only in a ragged last tile (P % 16 == 0 keeps a lane's DW
     // dwords inside one packet); with MG they still join the block's magic reduction
     const bool valid = colb < col_bytes;
-    if (!MG && !valid) continue;
+    if (!MG && !valid) return;
     const uint32_t sp = colb / P;
     const int64_t off = static_cast<int64_t>(sp) * 8 * P + (colb - sp * P);
     MagicLane ml;
@@ -525,7 +588,7 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
       }
     }
     if constexpr (MG) ml_commit(ml, a.magic_acc, s, K + R, static_cast<uint64_t>(a.size), static_cast<uint64_t>(off), P, red);
-  }
+  });
 }
 
 // ------------------------------------------------------------------ generic bitmatrix
@@ -980,10 +1043,10 @@ template <int R, int IT, bool BF, int VW>
 hipError_t bytewise_k(const ApplyArgs &a, hipStream_t st, int grid) {
   switch (a.K) {
 #define LSEC_BW_K(KK) \
-  case KK: return launch_kernel(&k_gf8_bytewise<R, KK, IT, BF, VW>, dim3(grid), dim3(kBlock), st, a);
+  case KK: return launch_tiled(&k_gf8_bytewise<R, KK, IT, BF, VW>, grid, st, a);
     LSEC_BW_K(4) LSEC_BW_K(6) LSEC_BW_K(8) LSEC_BW_K(10) LSEC_BW_K(12) LSEC_BW_K(16) LSEC_BW_K(20)
 #undef LSEC_BW_K
-    default: return launch_kernel(&k_gf8_bytewise<R, 0, IT, BF, VW>, dim3(grid), dim3(kBlock), st, a);
+    default: return launch_tiled(&k_gf8_bytewise<R, 0, IT, BF, VW>, grid, st, a);
   }
 }
 
@@ -999,7 +1062,7 @@ inline int bw_shape_vw(int shape) { return shape <= 1 ? 4 : 2; }
 template <int R>
 hipError_t dispatch_bytewise(const ApplyArgs &a, hipStream_t st, int grid, int shape) {
   if (a.accumulate) {  // a later input group of a wide stripe: generic K, 16 B per lane (shape 1)
-    return launch_kernel(&k_gf8_bytewise<R, 0, 1, true, 4, false, true>, dim3(grid), dim3(kBlock), st, a);
+    return launch_tiled(&k_gf8_bytewise<R, 0, 1, true, 4, false, true>, grid, st, a);
   }
   switch (shape) {
     case 1: return bytewise_k<R, 1, true, 4>(a, st, grid);
@@ -1016,12 +1079,12 @@ template <int R>
 hipError_t dispatch_bytewise_magic(const ApplyArgs &a, hipStream_t st, int grid) {
   switch (a.K) {
 #define LSEC_BWM_K(KK, IT) \
-  case KK: return launch_kernel(&k_gf8_bytewise<R, KK, IT, true, 4, true>, dim3(grid), dim3(kBlock), st, a);
+  case KK: return launch_tiled(&k_gf8_bytewise<R, KK, IT, true, 4, true>, grid, st, a);
     LSEC_BWM_K(4, 2) LSEC_BWM_K(6, 2) LSEC_BWM_K(8, 2) LSEC_BWM_K(10, 2) LSEC_BWM_K(12, 2) LSEC_BWM_K(16, 1) LSEC_BWM_K(20, 1)
 #undef LSEC_BWM_K
     default:
-      if (a.K >= 16) return launch_kernel(&k_gf8_bytewise<R, 0, 1, true, 4, true>, dim3(grid), dim3(kBlock), st, a);
-      else return launch_kernel(&k_gf8_bytewise<R, 0, 2, true, 4, true>, dim3(grid), dim3(kBlock), st, a);
+      if (a.K >= 16) return launch_tiled(&k_gf8_bytewise<R, 0, 1, true, 4, true>, grid, st, a);
+      else return launch_tiled(&k_gf8_bytewise<R, 0, 2, true, 4, true>, grid, st, a);
       break;
   }
 }
@@ -1029,15 +1092,15 @@ hipError_t dispatch_bytewise_magic(const ApplyArgs &a, hipStream_t st, int grid)
 template <int R>
 hipError_t dispatch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid, int dw) {
   if (a.magic_acc) {  // encode + stripe magic, one lane dword wide
-    return launch_kernel(&k_gf8_bitsliced<R, 0, 1, true>, dim3(grid), dim3(kBlock), st, a);
+    return launch_tiled(&k_gf8_bitsliced<R, 0, 1, true>, grid, st, a);
   }
   if (a.accumulate) {  // a later input group of a wide stripe, one lane dword wide
-    return launch_kernel(&k_gf8_bitsliced<R, 0, 1, false, true>, dim3(grid), dim3(kBlock), st, a);
+    return launch_tiled(&k_gf8_bitsliced<R, 0, 1, false, true>, grid, st, a);
   }
   switch (dw) {
-    case 4: return launch_kernel(&k_gf8_bitsliced<R, 0, 4>, dim3(grid), dim3(kBlock), st, a);
-    case 2: return launch_kernel(&k_gf8_bitsliced<R, 0, 2>, dim3(grid), dim3(kBlock), st, a);
-    default: return launch_kernel(&k_gf8_bitsliced<R, 0, 1>, dim3(grid), dim3(kBlock), st, a);
+    case 4: return launch_tiled(&k_gf8_bitsliced<R, 0, 4>, grid, st, a);
+    case 2: return launch_tiled(&k_gf8_bitsliced<R, 0, 2>, grid, st, a);
+    default: return launch_tiled(&k_gf8_bitsliced<R, 0, 1>, grid, st, a);
   }
 }
 

@@ -1095,6 +1095,10 @@ void lsec_set_kernel_variant(int bytewise_variant, int bitsliced_variant) {
   lsec::set_kernel_variant(bytewise_variant, bitsliced_variant);
 }
 
+void lsec_set_tile_sharing(int on) { lsec::set_tile_sharing(on != 0); }
+
+int lsec_tile_sharing(void) { return lsec::tile_sharing() ? 1 : 0; }
+
 
 // Self-test of the bitmatrix decode planner (test hook, not in include/; no GPU): for the
 // liberation-family plan (method, k, w) with m = 2, make_bit_decode's masks must equal those of

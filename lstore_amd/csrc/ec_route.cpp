@@ -53,6 +53,7 @@ const RouteTable &routes() {
     r.slot_pack_pool = static_cast<int>(env("LSEC_ZC_POOL", -1));
     r.slot_pack_inline = 2;
     r.staging_bytes = static_cast<size_t>(std::max(1L, env("LSEC_STAGING_MB", 128))) << 20;
+    r.dev_staging_bytes = static_cast<size_t>(std::max(1L, env("LSEC_DEV_STAGING_MB", 512))) << 20;
     r.slot_budget = static_cast<size_t>(std::max(0L, env("LSEC_ZC_SLOTS_MB", 1024))) << 20;
     r.dispatch_batch = 96u << 20;
     const long hw = std::max(1u, std::thread::hardware_concurrency());

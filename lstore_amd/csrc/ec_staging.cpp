@@ -148,17 +148,22 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   const int nin = static_cast<int>(in_ids.size()), nout = static_cast<int>(out_ids.size());
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
-  const size_t budget = routes().staging_bytes;
   const size_t per_col = static_cast<size_t>(nin + nout);  // staging bytes per column byte
+  // Batch geometry for a staging budget: whole stripes per slot when a stripe fits half the
+  // budget, else column blocks of one stripe (packet codes cut at super-packet boundaries)
   long long cb = C;
-  if (per_col * C > budget / 2) {
-    // packet codes must cut at super-packet boundaries (w * P bytes)
-    const long long align = packet_kind(kind) ? static_cast<long long>(p->w) * p->packet_size : 8192;
-    cb = static_cast<long long>(budget / 2 / per_col) / align * align;
-    if (cb < align) cb = align;
-    if (cb >= C) cb = C;
-  }
-  const int nb_max = cb < C ? 1 : static_cast<int>(std::max<size_t>(1, std::min<size_t>(nstripes, budget / 2 / (per_col * C))));
+  int nb_max = 1;
+  const auto geometry = [&](size_t budget) {
+    cb = C;
+    if (per_col * C > budget / 2) {
+      const long long align = packet_kind(kind) ? static_cast<long long>(p->w) * p->packet_size : 8192;
+      cb = static_cast<long long>(budget / 2 / per_col) / align * align;
+      if (cb < align) cb = align;
+      if (cb >= C) cb = C;
+    }
+    nb_max = cb < C ? 1 : static_cast<int>(std::max<size_t>(1, std::min<size_t>(nstripes, budget / 2 / (per_col * C))));
+  };
+  geometry(routes().staging_bytes);
   Staging *stg = acquire_staging(dev);
   if (!stg) return fail("cannot create staging streams");
   int rc = 0;
@@ -209,6 +214,10 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   // (profiles/r01_v28_host_trace.txt), but DMA of the same small registered runs is slower still:
   // kernel in + DMA out gave 17-30 GiB/s encode against 28-32 (profiles/r01_v28_kcopy_modes.txt).
   const bool out_by_kernel = by_kernel;
+  // DMA in place stages nothing on the host: the slots are device memory only, so they take the
+  // device budget, and wide stripes move whole (RS(20+6) at 4 MiB: 80 MiB runs instead of twenty
+  // 2.5 MiB column-block runs per stripe)
+  if (pinned && !by_kernel) geometry(std::max(rt.dev_staging_bytes, rt.staging_bytes));
   const size_t slot_bytes = per_col * static_cast<size_t>(cb) * nb_max;
   const auto t_loop0 = now();
   std::vector<DmaRun> runs;

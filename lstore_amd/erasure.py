@@ -79,7 +79,8 @@ EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan",
            "lsec_stripe_magic_dev", "lsec_segment_write", "lsec_segment_write_iov", "lsec_segment_encode_iov",
            "lsec_segment_straddle_bytes", "lsec_segment_read", "lsec_segment_inspect",
            "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count", "lsec_last_error", "lsec_plan_kernel",
-           "lsec_set_kernel_variant", "lsec_set_host_devices", "lsec_hbm_copy_dev", "lsec_hbm_mix_dev", "lsec_prepare_encode", "lsec_plan_jit", "lsec_device_numa")
+           "lsec_set_kernel_variant", "lsec_set_host_devices", "lsec_hbm_copy_dev", "lsec_hbm_mix_dev", "lsec_prepare_encode", "lsec_plan_jit", "lsec_device_numa",
+           "lsec_set_tile_sharing", "lsec_tile_sharing")
 
 # read / inspect flags and stripe states (include/lstore_ec.h)
 READ_PARANOID, MAGIC_LEGACY, INSPECT_FIX, MAX_DEVS = 1, 2, 4, 256
@@ -153,6 +154,9 @@ def lib():
     L.lsec_plan_kernel.argtypes = [P]
     L.lsec_set_kernel_variant.argtypes = [C.c_int, C.c_int]
     L.lsec_set_kernel_variant.restype = None
+    L.lsec_set_tile_sharing.argtypes = [C.c_int]
+    L.lsec_set_tile_sharing.restype = None
+    L.lsec_tile_sharing.restype = C.c_int
     L.lsec_set_host_devices.argtypes = [C.POINTER(C.c_int), C.c_int]
     L.lsec_hbm_copy_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_ulonglong, C.c_void_p]
     L.lsec_hbm_mix_dev.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_void_p]
@@ -544,6 +548,15 @@ def numa_for_bus(root: str, bus: str) -> tuple[int, list[int]]:
     if n < 0:
         raise ErasureError(f"lsec_test_numa_for_bus failed: {last_error()}")
     return node.value, list(cpus[:n])
+
+
+def set_tile_sharing(on: bool) -> None:
+    """lsec_set_tile_sharing: work-sharing tiles (True, the default) or static XCD eighths"""
+    lib().lsec_set_tile_sharing(1 if on else 0)
+
+
+def tile_sharing() -> bool:
+    return bool(lib().lsec_tile_sharing())
 
 
 def set_kernel_variant(bytewise: int = 0, bitsliced: int = 0) -> None:

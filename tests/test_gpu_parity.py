@@ -1125,3 +1125,82 @@ def _small_runs_case(method, k, m, size, n, shift, pinned):
         st[:, [1, k + m - 1]] = 0xA5
         p.decode_stripes(st, [1, k + m - 1])
         assert np.array_equal(st, full)
+
+
+# ---------------------------------------------------------------- work-sharing tiles
+@pytest.mark.parametrize("method,k,m,size,n", [
+    (L.REED_SOL_VAN, 6, 3, 1 << 20, 96),      # the headline kernel (bytewise, 8 KiB tiles)
+    (L.REED_SOL_VAN, 20, 6, 256 << 10, 64),   # K >= 16 bytewise shape, before any network binds
+    (L.CAUCHY_GOOD, 6, 3, 1 << 20, 64),       # bit-sliced
+    (L.REED_SOL_VAN, 6, 3, 1000, 3001),       # ragged tiles, more tiles than the persistent grid
+])
+def test_tile_sharing_is_bit_identical(cuda, method, k, m, size, n):
+    """Work-sharing tiles (ec_kernels.h): a persistent grid whose workgroups take tiles from an
+    atomic counter per XCD eighth and then help the other eighths.  Every tile must be coded
+    exactly once: encode, decode and the fused stripe magic give the same bytes as the static
+    eighths, launch after launch (the queue slots rotate and reset themselves), and match the
+    oracle on sampled stripes."""
+    import torch
+
+    from lstore_amd import erasure as E
+
+    g = torch.Generator(device=cuda).manual_seed(11)
+    d = torch.randint(0, 256, (n, k, size), dtype=torch.uint8, device=cuda, generator=g)
+    outs = {}
+    try:
+        with L.Plan.for_chunk(method, k, m, size) as p:
+            for on in (False, True, True, False, True):
+                E.set_tile_sharing(on)
+                par = torch.zeros((n, m, size), dtype=torch.uint8, device=cuda)
+                mg = torch.zeros((n, 4), dtype=torch.uint8, device=cuda)
+                p.encode_magic_dev(d, par, mg)
+                rb = torch.zeros((n, 2, size), dtype=torch.uint8, device=cuda)
+                p.decode_dev(d, par, [0, k], out=rb)
+                torch.cuda.synchronize()
+                assert torch.equal(rb[:, 0], d[:, 0]) and torch.equal(rb[:, 1], par[:, 0]), on
+                if on in outs:
+                    assert torch.equal(par, outs[on][0]) and torch.equal(mg, outs[on][1]), on
+                outs[on] = (par, mg)
+            assert torch.equal(outs[True][0], outs[False][0]) and torch.equal(outs[True][1], outs[False][1])
+            hd, hp = d.cpu().numpy(), outs[True][0].cpu().numpy()
+            for s in (0, n // 2, n - 1):
+                assert_same(hp[s], O.encode(method, hd[s], m, p.packet_size))
+    finally:
+        E.set_tile_sharing(True)
+
+
+def test_tile_sharing_concurrent_streams(cuda):
+    """Launches from several threads on their own streams at once: each takes its own queue slot
+    (one ring per device), so concurrent launches never share counters."""
+    import threading
+
+    import torch
+
+    k, m, size, n = 6, 3, 256 << 10, 128
+    g = torch.Generator(device=cuda).manual_seed(5)
+    d = torch.randint(0, 256, (n, k, size), dtype=torch.uint8, device=cuda, generator=g)
+    with L.Plan.for_chunk(L.REED_SOL_VAN, k, m, size) as p:
+        want = torch.empty((n, m, size), dtype=torch.uint8, device=cuda)
+        p.encode_dev(d, want)
+        torch.cuda.synchronize()
+        errs = []
+
+        def worker(i):
+            try:
+                s = torch.cuda.Stream()
+                with torch.cuda.stream(s):
+                    for _ in range(20):
+                        par = torch.empty((n, m, size), dtype=torch.uint8, device=cuda)
+                        p.encode_dev(d, par, stream=s)
+                        s.synchronize()
+                        if not torch.equal(par, want):
+                            errs.append(i)
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+
+        ts = [threading.Thread(target=worker, args=(i,)) for i in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert errs == []
