@@ -255,10 +255,12 @@ const char *lsec_last_error(void);           /* thread-local message of the last
  * 0 = no GPU kernel (calls fail with -1) */
 int lsec_plan_kernel(lio_erasure_plan_t *plan);
 void lsec_set_kernel_variant(int bytewise_variant, int bitsliced_variant);  /* tuning experiments */
-/* Work-sharing tiles for the streaming kernels (default on; LSEC_TILES=static starts it off):
- * 1 = persistent grid, each XCD takes tiles from its own eighth and then helps the others;
- * 0 = each XCD its static eighth.  For A/B runs; results are identical either way. */
-void lsec_set_tile_sharing(int on);
+/* How the streaming kernels deal their tiles to the 8 XCDs (LSEC_TILES=static|shared|tail picks
+ * the start value; default tail): 0 = each XCD its static eighth; 1 = persistent grid, each XCD
+ * takes tiles from its own eighth through an atomic counter and then helps the others; 2 = the
+ * first 7/8 of each eighth static, the rest shared.  For A/B runs; results are identical in every
+ * mode. */
+void lsec_set_tile_sharing(int mode);
 int lsec_tile_sharing(void);
 /* Measurement probe, not part of the coding path: enqueue a streaming device copy dst <- src
  * (bytes a multiple of 16, 16-byte aligned device pointers) on `stream` with the coding kernels'

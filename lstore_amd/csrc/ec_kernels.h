@@ -88,6 +88,9 @@ struct ApplyArgs {
   unsigned long long *magic_acc;  // encode only (bytewise, bitsliced): fused stripe magic over the K inputs then the
                                   // R outputs (2 x u64 per stripe, zeroed), see MagicArgs
   unsigned *tiles;        // work-sharing tile queue slot (tile_queue_slot), or null: each XCD its static eighth
+  uint32_t tiles_pre;     // with a slot: the tiles of each eighth dealt statically before the sharing starts
+  unsigned long long *stamps;  // measurement only (lsec_test_set_stamps): each workgroup's end time, or null
+  uint32_t nstamps;
   ShardRef in[kMaxK];
   ShardRef out[kMaxR];
 };
@@ -105,8 +108,16 @@ struct ApplyArgs {
 constexpr int kTileQueueLine = 32;  // unsigned words per counter (a 128-B line each)
 constexpr int kTileQueueWords = 9 * kTileQueueLine;
 constexpr int kTileQueueRing = 4096;
-// a slot on the device of stream st; null: tile sharing off or unavailable (the static eighths serve)
-unsigned *tile_queue_slot(hipStream_t st);
+// a slot on the device of stream st for a launch of ntiles tiles; null: tile sharing off, the
+// launch small (fewer than kTileQueueMinTiles), or no slot available (the static eighths serve)
+constexpr uint64_t kTileQueueMinTiles = 16384;
+unsigned *tile_queue_slot(hipStream_t st, uint64_t ntiles);
+// with tile sharing on, the tiles of each eighth (of ntiles) dealt statically, one per block,
+// before the sharing blocks take the rest (LSEC_TILES=shared: none; the default keeps 7/8)
+uint32_t tiles_prefix(uint32_t ntiles);
+// measurement hook: the buffer launch_tiled hands its kernels for per-workgroup end times
+unsigned long long *launch_stamps(uint32_t *n);
+void set_launch_stamps(unsigned long long *p, uint32_t n);
 // the persistent grid of `kernel` on st's device (its resident workgroups of kBlock threads,
 // times the CUs), at most `grid`; 0 when the runtime cannot say
 int persistent_grid(const void *kernel, int grid, hipStream_t st);
@@ -210,8 +221,8 @@ void make_word_cell(uint32_t c, int w, uint32_t *out);
 
 // Variant selection knobs for experiments: 0 = default
 void set_kernel_variant(int bytewise_variant, int bitsliced_variant);
-void set_tile_sharing(bool on);  // lsec_set_tile_sharing
-bool tile_sharing();
+void set_tile_mode(int mode);  // lsec_set_tile_sharing: 0 static, 1 shared, 2 static prefix + shared tail
+int tile_mode();
 int bytewise_variant();  // != 0: a forced bytewise shape (also keeps wide codes off their XOR networks)
 int bitsliced_variant();  // != 0: a forced bit-sliced / wordwise variant (also keeps w = 16 / 32 RS off its XOR network)
 

@@ -29,17 +29,30 @@ unsigned *g_queue[kQueueDevs];
 std::atomic<uint32_t> g_queue_next[kQueueDevs];
 int g_cus[kQueueDevs];
 
-std::atomic<int> g_tiles_shared{-1};  // -1: not read from LSEC_TILES yet
+// tile mode: 0 static eighths, 1 all tiles shared, 2 a static prefix and a shared tail
+std::atomic<int> g_tiles_mode{-1};  // -1: not read from LSEC_TILES yet
 
-bool tiles_shared() {
-  int v = g_tiles_shared.load(std::memory_order_relaxed);
+int tiles_mode() {
+  int v = g_tiles_mode.load(std::memory_order_relaxed);
   if (v < 0) {
     const char *e = getenv("LSEC_TILES");
-    int want = e && std::strcmp(e, "static") == 0 ? 0 : 1;
-    g_tiles_shared.compare_exchange_strong(v, want);
-    v = g_tiles_shared.load(std::memory_order_relaxed);
+    const int want = !e ? 2 : std::strcmp(e, "static") == 0 ? 0 : std::strcmp(e, "shared") == 0 ? 1 : 2;
+    g_tiles_mode.compare_exchange_strong(v, want);
+    v = g_tiles_mode.load(std::memory_order_relaxed);
   }
-  return v != 0;
+  return v;
+}
+
+bool tiles_shared() { return tiles_mode() != 0; }
+
+// the static prefix's share of each eighth, in 1/64ths (LSEC_TILES_PRE_64THS, A/B runs)
+uint32_t prefix_64ths() {
+  static const uint32_t v = [] {
+    const char *e = getenv("LSEC_TILES_PRE_64THS");
+    const long x = e ? atol(e) : 56;
+    return static_cast<uint32_t>(std::max(0L, std::min(64L, x)));
+  }();
+  return v;
 }
 
 template <typename F>
@@ -80,8 +93,24 @@ int stream_device(hipStream_t st) {
 
 }  // namespace
 
-unsigned *tile_queue_slot(hipStream_t st) {
-  if (!tiles_shared()) return nullptr;
+namespace {
+std::atomic<unsigned long long *> g_stamps{nullptr};
+std::atomic<uint32_t> g_nstamps{0};
+}  // namespace
+
+unsigned long long *launch_stamps(uint32_t *n) {
+  *n = g_nstamps.load(std::memory_order_relaxed);
+  return g_stamps.load(std::memory_order_relaxed);
+}
+
+void set_launch_stamps(unsigned long long *p, uint32_t n) {
+  g_nstamps.store(p ? n : 0, std::memory_order_relaxed);
+  g_stamps.store(p, std::memory_order_relaxed);
+}
+
+unsigned *tile_queue_slot(hipStream_t st, uint64_t ntiles) {
+  // small launches (a stripe or a few) keep the static eighths: one tile per block, no counters
+  if (!tiles_shared() || ntiles < kTileQueueMinTiles) return nullptr;
   const int dev = stream_device(st);
   if (dev < 0 || dev >= kQueueDevs) return nullptr;
   std::call_once(g_queue_once[dev], [dev] {
@@ -143,9 +172,15 @@ int persistent_grid(const void *kernel, int grid, hipStream_t st) {
   return pg;
 }
 
-void set_tile_sharing(bool on) { g_tiles_shared.store(on ? 1 : 0, std::memory_order_relaxed); }
+void set_tile_mode(int mode) { g_tiles_mode.store(std::max(0, std::min(2, mode)), std::memory_order_relaxed); }
 
-bool tile_sharing() { return tiles_shared(); }
+int tile_mode() { return tiles_mode(); }
+
+uint32_t tiles_prefix(uint32_t ntiles) {
+  if (tiles_mode() != 2) return 0;
+  const uint64_t per = (static_cast<uint64_t>(ntiles) + 7) / 8;
+  return static_cast<uint32_t>(per * prefix_64ths() / 64);
+}
 
 void set_kernel_variant(int bw, int bs) {
   g_bw_variant = bw;
@@ -335,10 +370,11 @@ __global__ __launch_bounds__(kBlock) void k_gather(const GatherPiece *list, char
 // HBM probe: a plain streaming copy with the coding kernels' memory shape (one 8 KiB tile
 // per block, XCD-contiguous block order, 2 x 16 B non-temporal loads and stores per lane).
 // bench.py times it beside the encode as this box's practical read+write ceiling.
-__global__ __launch_bounds__(kBlock) void k_hbm_copy(uint64_t dst, uint64_t src, uint64_t n16, unsigned *tiles) {
+__global__ __launch_bounds__(kBlock) void k_hbm_copy(uint64_t dst, uint64_t src, uint64_t n16, unsigned *tiles,
+                                                    uint32_t tiles_pre) {
   constexpr int kIt = 2;
   const uint32_t ntiles = static_cast<uint32_t>((n16 + kBlock * kIt - 1) / (kBlock * kIt));
-  for_tiles(ntiles, tiles, [&](uint64_t t) {
+  for_tiles(ntiles, tiles, tiles_pre, [&](uint64_t t) {
     const uint64_t i0 = t * kBlock * kIt + threadIdx.x;
     u32x4 v[kIt];
 #pragma unroll
@@ -363,7 +399,7 @@ __global__ __launch_bounds__(kBlock) void k_hbm_mix(ApplyArgs a) {
   const int64_t C = a.size;
   const uint32_t tps = static_cast<uint32_t>((C + kTile - 1) / kTile);
   const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
-  for_tiles(ntiles, a.tiles, [&](uint32_t t) {
+  for_tiles(ntiles, a.tiles, a.tiles_pre, [&](uint32_t t) {
     const uint32_t s = t / tps;
     const int64_t off0 = static_cast<int64_t>(t - s * tps) * kTile + threadIdx.x * 16;
     u32x4 acc[kIt] = {0u, 0u};
@@ -458,14 +494,19 @@ hipError_t launch_hbm_copy(void *dst, const void *src, uint64_t bytes, hipStream
   if (ntiles == 0) return hipSuccess;
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   int grid = default_grid(ntiles);
-  unsigned *q = tile_queue_slot(st);
+  unsigned *q = tile_queue_slot(st, ntiles);
+  uint32_t pre = 0;
   if (q) {
     const int pg = persistent_grid(reinterpret_cast<const void *>(&k_hbm_copy), grid, st);
-    if (pg > 0) grid = pg;
-    else q = nullptr;
+    if (pg > 0) {
+      pre = tiles_prefix(static_cast<uint32_t>(grid));
+      grid = static_cast<int>(8 * pre) + pg;
+    } else {
+      q = nullptr;
+    }
   }
   return launch_kernel(&k_hbm_copy, dim3(grid), dim3(kBlock), st, reinterpret_cast<uint64_t>(dst),
-                     reinterpret_cast<uint64_t>(src), n16, q);
+                     reinterpret_cast<uint64_t>(src), n16, q, pre);
 }
 
 hipError_t launch_hbm_mix(const ApplyArgs &a, hipStream_t st) {

@@ -100,50 +100,62 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
   return xcd * per + min(xcd, rem) + (b >> 3);
 }
 
-// Every tile t < ntiles to body(t) exactly once, body's t uniform over the workgroup.  q null:
-// the grid strides over the tiles from its XCD-contiguous start (one tile per block when the grid
-// is the tile count).  q a tile queue slot (ec_kernels.h, "Work-sharing tiles"): the grid is
-// persistent; a workgroup takes G consecutive tiles at a time (a grab) from its own XCD's eighth
-// of the grabs, then from the other eighths'.  Thread 0 issues the atomic for the next grab before
-// the current grab's tiles and reads its result after them, so the counter's round trip hides
-// behind the tiles' loads; it posts the index in one of two LDS words (never one a wave has yet to
-// read: that wave has not passed the barrier after its read), and readfirstlane keeps the loop
-// exit uniform.
+// Every tile t < ntiles to body(t) exactly once, body's t uniform over the workgroup.
+//   q null: the grid strides over the tiles from its XCD-contiguous start (one tile per block
+//   when the grid is the tile count): each XCD its static eighth.
+//   q a tile queue slot (ec_kernels.h, "Work-sharing tiles"): each eighth's first `pre` tiles go
+//   one per block to blocks 0 .. 8*pre-1 (block b on XCD b % 8, as the static form), and the
+//   blocks after those share the rest: each takes G consecutive tiles at a time (a grab) from its
+//   own XCD's remainder, then from the other eighths'.  pre = 0: all tiles are shared.  Thread 0
+//   issues the atomic for the next grab as soon as it has the current one, so the counter's round
+//   trip hides behind the grab's tiles; it posts the grab in one of two LDS words (never one a wave
+//   has yet to read: that wave has not passed the barrier after its read), and readfirstlane keeps
+//   the loop uniform.  One call site of body for every form: the kernels' code is not repeated.
 template <int G = 1, typename Body>
-__device__ __forceinline__ void for_tiles(uint32_t ntiles, unsigned *q, Body &&body) {
-  if (q == nullptr) {
-    for (uint32_t t = xcd_remap(blockIdx.x, gridDim.x); t < ntiles; t += gridDim.x) body(t);
-    return;
-  }
+__device__ __forceinline__ void for_tiles(uint32_t ntiles, unsigned *q, uint32_t pre, Body &&body) {
   __shared__ uint32_t next[2];
-  const uint32_t units = (ntiles + G - 1) / G, per = (units + 7) >> 3, xcd = blockIdx.x & 7;
+  const uint32_t per = (ntiles + 7) >> 3, xcd = blockIdx.x & 7;
+  const bool sharing = q != nullptr && blockIdx.x >= 8 * pre;  // block-uniform
+  const uint32_t rest = per - pre, grabs = (rest + G - 1) / G;  // each eighth's shared tiles, grabs
   uint32_t k = 0, pend = 0, it = 0;  // thread 0: eighths done, the counter value in flight
-  const auto take = [&]() -> uint32_t {  // thread 0: the grab `pend` names, or `units` when all are gone
+  const auto take = [&]() -> uint32_t {  // thread 0: first tile of the grab `pend` names, or ntiles
     for (;;) {
-      const uint32_t e = (xcd + k) & 7, u = e * per + pend;
-      if (pend < per && u < units) return u;
-      if (++k == 8) return units;
+      const uint32_t t = ((xcd + k) & 7) * per + pre + pend * G;
+      if (pend < grabs && t < ntiles) return t;
+      if (++k == 8) return ntiles;
       pend = atomicAdd(q + kTileQueueLine * ((xcd + k) & 7), 1u);
     }
   };
-  if (threadIdx.x == 0) {
-    pend = atomicAdd(q + kTileQueueLine * xcd, 1u);
-    next[0] = take();
+  uint32_t t, end, step = 1;
+  if (q == nullptr) {
+    t = xcd_remap(blockIdx.x, gridDim.x);
+    end = ntiles;
+    step = gridDim.x;
+  } else if (!sharing) {  // the static prefix: one tile
+    t = xcd * per + (blockIdx.x >> 3);
+    end = min(ntiles, t + 1);
+  } else {
+    t = end = 0;  // the first grab comes below
   }
-  __syncthreads();
-  uint32_t u = __builtin_amdgcn_readfirstlane(next[0]);
-  while (u < units) {
-    if (threadIdx.x == 0) pend = atomicAdd(q + kTileQueueLine * ((xcd + k) & 7), 1u);  // the next grab
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-      if (G == 1 || u * G + g < ntiles) body(u * G + g);
-    ++it;
-    if (threadIdx.x == 0) next[it & 1] = take();
-    __syncthreads();
-    u = __builtin_amdgcn_readfirstlane(next[it & 1]);
+  for (;;) {
+    if (t >= end) {
+      if (!sharing) break;
+      if (threadIdx.x == 0) {
+        if (it == 0) pend = atomicAdd(q + kTileQueueLine * xcd, 1u);
+        next[it & 1] = take();
+      }
+      __syncthreads();
+      t = __builtin_amdgcn_readfirstlane(next[it & 1]);
+      ++it;
+      if (t >= ntiles) break;
+      end = min(min(ntiles, (t / per + 1) * per), t + G);  // a grab stays inside its eighth
+      if (threadIdx.x == 0) pend = atomicAdd(q + kTileQueueLine * ((xcd + k) & 7), 1u);  // the next grab
+    }
+    body(t);
+    t += step;
   }
-  // the launch's last workgroup leaves the slot zeroed for its next use (kTileQueueRing launches on)
-  if (threadIdx.x == 0 && atomicAdd(q + kTileQueueLine * 8, 1u) == gridDim.x - 1)
+  // the launch's last sharing block leaves the slot zeroed for its next use (kTileQueueRing launches on)
+  if (sharing && threadIdx.x == 0 && atomicAdd(q + kTileQueueLine * 8, 1u) == gridDim.x - 8 * pre - 1)
     for (int e = 0; e <= 8; ++e) atomicExch(q + kTileQueueLine * e, 0u);
 }
 
@@ -151,13 +163,18 @@ __device__ __forceinline__ void for_tiles(uint32_t ntiles, unsigned *q, Body &&b
 // persistent grid when tile sharing is on (ec_kernels.h), else on `grid` blocks over static eighths.
 template <typename Kern>
 hipError_t launch_tiled(Kern *k, int grid, hipStream_t st, ApplyArgs a) {
-  a.tiles = tile_queue_slot(st);
+  a.stamps = launch_stamps(&a.nstamps);
+  a.tiles = tile_queue_slot(st, static_cast<uint64_t>(grid));
+  a.tiles_pre = 0;
   if (a.tiles) {
     const int pg = persistent_grid(reinterpret_cast<const void *>(k), grid, st);
-    if (pg > 0)
-      grid = pg;
-    else
+    if (pg > 0) {
+      // `grid` is the tile count here (one tile per block in the static form)
+      a.tiles_pre = tiles_prefix(static_cast<uint32_t>(grid));
+      grid = static_cast<int>(8 * a.tiles_pre) + pg;
+    } else {
       a.tiles = nullptr;
+    }
   }
   return launch_kernel(k, dim3(grid), dim3(kBlock), st, a);
 }
@@ -387,7 +404,7 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
   ConstCell *cells = const_cells(a.cells);
 
   // grabs of about 8 KiB per shard (the single-erasure decode's 2 KiB tiles go 4 at a time)
-  for_tiles<(kTile >= 8192 ? 1 : 8192 / kTile)>(ntiles, a.tiles, [&](uint32_t t) {
+  for_tiles<(kTile >= 8192 ? 1 : 8192 / kTile)>(ntiles, a.tiles, a.tiles_pre, [&](uint32_t t) {
     const uint32_t s = t / tiles_per_stripe;
     const int64_t off0 = static_cast<int64_t>(t - s * tiles_per_stripe) * kTile + threadIdx.x * kLane;
     const bool full = (static_cast<int64_t>(t - s * tiles_per_stripe) + 1) * kTile <= C;  // wave-uniform
@@ -508,6 +525,10 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bytewise(ApplyArgs a) {
     }
   }
   bytewise_tiles<R, KC, IT, BF, VW, MG, false, ACC>(a);
+  if (a.stamps) {  // measurement only: when this workgroup finished (s_memrealtime, 100 MHz)
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < a.nstamps) a.stamps[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 // ------------------------------------------------------------------ bitsliced
@@ -526,7 +547,7 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
   const uint32_t ntiles = tiles_per_stripe * static_cast<uint32_t>(a.nstripes);
   ConstCell *cells = const_cells(a.cells);
 
-  for_tiles(ntiles, a.tiles, [&](uint32_t t) {
+  for_tiles(ntiles, a.tiles, a.tiles_pre, [&](uint32_t t) {
     const uint32_t s = t / tiles_per_stripe;
     const uint32_t colb = (t - s * tiles_per_stripe) * kTile + threadIdx.x * (4 * DW);
     // lanes past the end occur only in a ragged last tile (P % 16 == 0 keeps a lane's DW

@@ -1095,9 +1095,15 @@ void lsec_set_kernel_variant(int bytewise_variant, int bitsliced_variant) {
   lsec::set_kernel_variant(bytewise_variant, bitsliced_variant);
 }
 
-void lsec_set_tile_sharing(int on) { lsec::set_tile_sharing(on != 0); }
+void lsec_set_tile_sharing(int mode) { lsec::set_tile_mode(mode); }
 
-int lsec_tile_sharing(void) { return lsec::tile_sharing() ? 1 : 0; }
+int lsec_tile_sharing(void) { return lsec::tile_mode(); }
+
+// Test hook, not in include/: device buffer of n u64 for the bytewise kernels' per-workgroup end
+// times (s_memrealtime) in the following launches, or NULL to stop (tools/xcd_stamps.py).
+void lsec_test_set_stamps(void *dev_buf, unsigned n) {
+  lsec::set_launch_stamps(static_cast<unsigned long long *>(dev_buf), n);
+}
 
 
 // Self-test of the bitmatrix decode planner (test hook, not in include/; no GPU): for the

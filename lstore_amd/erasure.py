@@ -550,13 +550,18 @@ def numa_for_bus(root: str, bus: str) -> tuple[int, list[int]]:
     return node.value, list(cpus[:n])
 
 
-def set_tile_sharing(on: bool) -> None:
-    """lsec_set_tile_sharing: work-sharing tiles (True, the default) or static XCD eighths"""
-    lib().lsec_set_tile_sharing(1 if on else 0)
+TILES_STATIC, TILES_SHARED, TILES_TAIL = 0, 1, 2
 
 
-def tile_sharing() -> bool:
-    return bool(lib().lsec_tile_sharing())
+def set_tile_sharing(mode) -> None:
+    """lsec_set_tile_sharing: TILES_STATIC (each XCD its eighth), TILES_SHARED (all tiles through
+    per-XCD counters with stealing) or TILES_TAIL (the default: a static 7/8, the rest shared);
+    True / False select TILES_SHARED / TILES_STATIC"""
+    lib().lsec_set_tile_sharing(int(mode))
+
+
+def tile_sharing() -> int:
+    return int(lib().lsec_tile_sharing())
 
 
 def set_kernel_variant(bytewise: int = 0, bitsliced: int = 0) -> None:

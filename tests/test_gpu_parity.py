@@ -1128,18 +1128,19 @@ def _small_runs_case(method, k, m, size, n, shift, pinned):
 
 
 # ---------------------------------------------------------------- work-sharing tiles
+# (launches of at least kTileQueueMinTiles = 16384 tiles take the queue)
 @pytest.mark.parametrize("method,k,m,size,n", [
-    (L.REED_SOL_VAN, 6, 3, 1 << 20, 96),      # the headline kernel (bytewise, 8 KiB tiles)
-    (L.REED_SOL_VAN, 20, 6, 256 << 10, 64),   # K >= 16 bytewise shape, before any network binds
-    (L.CAUCHY_GOOD, 6, 3, 1 << 20, 64),       # bit-sliced
-    (L.REED_SOL_VAN, 6, 3, 1000, 3001),       # ragged tiles, more tiles than the persistent grid
+    (L.REED_SOL_VAN, 6, 3, 1 << 20, 160),     # the headline kernel (bytewise, 8 KiB tiles): 20480 tiles
+    (L.REED_SOL_VAN, 20, 6, 256 << 10, 300),  # K >= 16 bytewise shape (4 KiB tiles), before any network binds
+    (L.CAUCHY_GOOD, 6, 3, 1 << 20, 160),      # bit-sliced (1 KiB of packet columns per tile)
+    (L.REED_SOL_VAN, 6, 3, 1000, 20001),      # ragged tiles, one per stripe; more than the persistent grid
 ])
 def test_tile_sharing_is_bit_identical(cuda, method, k, m, size, n):
-    """Work-sharing tiles (ec_kernels.h): a persistent grid whose workgroups take tiles from an
-    atomic counter per XCD eighth and then help the other eighths.  Every tile must be coded
-    exactly once: encode, decode and the fused stripe magic give the same bytes as the static
-    eighths, launch after launch (the queue slots rotate and reset themselves), and match the
-    oracle on sampled stripes."""
+    """Work-sharing tiles (ec_kernels.h): workgroups that take tiles from an atomic counter per XCD
+    eighth and then help the other eighths, for all tiles (shared) or after a static 7/8 of each
+    eighth (tail).  Every tile must be coded exactly once: encode, decode and the fused stripe magic
+    give the same bytes in every mode, launch after launch (the queue slots rotate and reset
+    themselves), and match the oracle on sampled stripes."""
     import torch
 
     from lstore_amd import erasure as E
@@ -1149,7 +1150,7 @@ def test_tile_sharing_is_bit_identical(cuda, method, k, m, size, n):
     outs = {}
     try:
         with L.Plan.for_chunk(method, k, m, size) as p:
-            for on in (False, True, True, False, True):
+            for on in (E.TILES_STATIC, E.TILES_SHARED, E.TILES_TAIL, E.TILES_SHARED, E.TILES_STATIC, E.TILES_TAIL):
                 E.set_tile_sharing(on)
                 par = torch.zeros((n, m, size), dtype=torch.uint8, device=cuda)
                 mg = torch.zeros((n, 4), dtype=torch.uint8, device=cuda)
@@ -1161,12 +1162,14 @@ def test_tile_sharing_is_bit_identical(cuda, method, k, m, size, n):
                 if on in outs:
                     assert torch.equal(par, outs[on][0]) and torch.equal(mg, outs[on][1]), on
                 outs[on] = (par, mg)
-            assert torch.equal(outs[True][0], outs[False][0]) and torch.equal(outs[True][1], outs[False][1])
-            hd, hp = d.cpu().numpy(), outs[True][0].cpu().numpy()
+            for mode in (E.TILES_SHARED, E.TILES_TAIL):
+                assert torch.equal(outs[mode][0], outs[E.TILES_STATIC][0]), mode
+                assert torch.equal(outs[mode][1], outs[E.TILES_STATIC][1]), mode
+            hd, hp = d.cpu().numpy(), outs[E.TILES_TAIL][0].cpu().numpy()
             for s in (0, n // 2, n - 1):
                 assert_same(hp[s], O.encode(method, hd[s], m, p.packet_size))
     finally:
-        E.set_tile_sharing(True)
+        E.set_tile_sharing(E.TILES_TAIL)
 
 
 def test_tile_sharing_concurrent_streams(cuda):
@@ -1176,7 +1179,7 @@ def test_tile_sharing_concurrent_streams(cuda):
 
     import torch
 
-    k, m, size, n = 6, 3, 256 << 10, 128
+    k, m, size, n = 6, 3, 256 << 10, 600  # 19200 tiles per launch: the queue path
     g = torch.Generator(device=cuda).manual_seed(5)
     d = torch.randint(0, 256, (n, k, size), dtype=torch.uint8, device=cuda, generator=g)
     with L.Plan.for_chunk(L.REED_SOL_VAN, k, m, size) as p:

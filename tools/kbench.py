@@ -37,6 +37,10 @@ CONFIGS = {
     "rs124": (L.REED_SOL_VAN, 12, 4, 1 << 20),
     "rs84": (L.REED_SOL_VAN, 8, 4, 1 << 20),
     "cg206": (L.CAUCHY_GOOD, 20, 6, 256 << 10),
+    # the c5 points under 0.70 in round 4 (r04_v15_sweep_c5.jsonl)
+    "rs84c8": (L.REED_SOL_VAN, 8, 4, 8 << 20),
+    "rs124c4": (L.REED_SOL_VAN, 12, 4, 4 << 20),
+    "cg206c2": (L.CAUCHY_GOOD, 20, 6, 2 << 20),
     # wide fields (w = 16 / 32): transposed bit-sliced RS, bit-sliced Cauchy
     "rs63w16": (L.REED_SOL_VAN, 6, 3, 1 << 20, 16),
     "rs63w32": (L.REED_SOL_VAN, 6, 3, 1 << 20, 32),

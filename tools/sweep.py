@@ -40,6 +40,8 @@ def link_rates(torch, dev, nbytes=1 << 30, reps=5):
             torch.cuda.synchronize()
             t.append(time.perf_counter() - t0)
         best[name + "_GBps"] = round(nbytes / min(t) / 1e9, 2)
+    # (both directions at once: tools/probes/duplex_probe.cpp -- torch copies on two streams
+    # serialise and read as half the rate each, which the link does not)
     del h, d
     torch.cuda.empty_cache()
     return best

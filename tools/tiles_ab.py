@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Work-sharing tiles A/B (lsec_set_tile_sharing): the headline RS(6+3) 1 MiB encode and
-single-erasure decode over the SAME fresh allocation, static XCD eighths and shared tiles timed
-alternately, over several fresh allocations; parity and rebuilt shards compared between the modes.
+single-erasure decode over the SAME fresh allocation, static XCD eighths, all tiles shared and a
+static prefix with a shared tail timed alternately, over several fresh allocations; parity and
+rebuilt shards compared between the modes.
 
 python tools/tiles_ab.py [--trials 4] [--rounds 4] [--reps 5] [--method reed_sol_van --k 6 --m 3 --chunk 1048576]
 """
@@ -46,12 +47,12 @@ def main():
         p = torch.empty((N, m, C), dtype=torch.uint8, device=dev)
         r = torch.empty((N, 1, C), dtype=torch.uint8, device=dev)
         del spacer
-        times = {"static": ([], []), "shared": ([], [])}
+        times = {"static": ([], []), "shared": ([], []), "tail": ([], [])}
         ref = None
         same = True
         for rnd in range(a.rounds):
-            for mode in ("static", "shared"):
-                E.set_tile_sharing(mode == "shared")
+            for mode in ("static", "shared", "tail"):
+                E.set_tile_sharing({"static": E.TILES_STATIC, "shared": E.TILES_SHARED, "tail": E.TILES_TAIL}[mode])
                 plan.encode_dev(d, p)
                 plan.decode_dev(d, p, [0], out=r)
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
@@ -78,12 +79,13 @@ def main():
             rec[mode] = {"encode_ms": round(te_m, 4), "decode_ms": round(td_m, 4),
                          "encode_frac": round((k + m) * C * N / (te_m / 1e3) / 8e12, 4),
                          "decode_frac": round((k + 1) * C * N / (td_m / 1e3) / 8e12, 4)}
-        rec["encode_gain"] = round(rec["static"]["encode_ms"] / rec["shared"]["encode_ms"], 4)
-        rec["decode_gain"] = round(rec["static"]["decode_ms"] / rec["shared"]["decode_ms"], 4)
+        for mode in ("shared", "tail"):
+            rec[mode]["encode_gain"] = round(rec["static"]["encode_ms"] / rec[mode]["encode_ms"], 4)
+            rec[mode]["decode_gain"] = round(rec["static"]["decode_ms"] / rec[mode]["decode_ms"], 4)
         out.append(rec)
         print(json.dumps(rec), flush=True)
         del d, p, r
-    E.set_tile_sharing(True)
+    E.set_tile_sharing(E.TILES_TAIL)
     if a.json:
         with open(a.json, "w") as f:
             for rec in out:
