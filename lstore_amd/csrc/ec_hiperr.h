@@ -10,9 +10,11 @@ namespace lsec {
 // hold an error of the caller's own that the caller has not read yet.  Runtime calls that can fail
 // (by design: hipHostGetFlags on a registered range, an address-range query, a registration the
 // runtime refuses; or an allocation that fails) go through quiet(): inline when the caller's slot
-// is clear (the engine then clears the error it caused itself), and on a short-lived engine thread
-// (a slot of its own) when the caller has an error pending, so that the caller's error stays where
-// the caller left it.  Defined in ec_pinning.cpp.
+// is clear (the engine then clears the error it caused itself), and on the engine's one helper
+// thread (a slot of its own; it takes the caller's current device first) when the caller has an
+// error pending, so that the caller's error stays where the caller left it.  A caller that leaves
+// an error unread pays a thread hand-off (a few microseconds) per such call until it reads it.
+// Defined in ec_pinning.cpp.
 hipError_t quiet(const std::function<hipError_t()> &f);
 
 }  // namespace lsec

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstring>
 #include <map>
@@ -19,6 +20,65 @@
 
 namespace lsec {
 
+namespace {
+
+// The engine thread that runs quiet()'s calls while a caller's error is pending: one persistent
+// thread (a hand-off costs a few microseconds; a thread per call cost tens), started at first need
+// and left running for the process's life.
+class QuietThread {
+ public:
+  static QuietThread &get() {
+    static QuietThread *t = new QuietThread();  // leaked: callers may still use it during exit
+    return *t;
+  }
+  hipError_t run(const std::function<hipError_t()> &f) {
+    // the caller's current device, so that device-relative calls (module loads, allocations) act
+    // where they would have on the caller's thread (a successful call leaves the caller's error)
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [this] { return job_ == nullptr; });  // one call at a time
+    job_ = &f;
+    dev_ = dev;
+    ++seq_;
+    const unsigned long long mine = seq_;
+    cv_.notify_one();
+    done_cv_.wait(lk, [&] { return finished_ == mine; });
+    const hipError_t e = result_;
+    job_ = nullptr;
+    done_cv_.notify_all();
+    return e;
+  }
+
+ private:
+  QuietThread() { std::thread([this] { loop(); }).detach(); }
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [this] { return job_ != nullptr && finished_ != seq_; });
+      const std::function<hipError_t()> *f = job_;
+      const unsigned long long s = seq_;
+      const int dev = dev_;
+      lk.unlock();
+      if (dev >= 0 && hipSetDevice(dev) != hipSuccess) (void)hipGetLastError();
+      hipError_t e = (*f)();
+      if (e != hipSuccess) (void)hipGetLastError();  // this thread's slot: the error is the engine's
+      lk.lock();
+      result_ = e;
+      finished_ = s;
+      done_cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<hipError_t()> *job_ = nullptr;
+  unsigned long long seq_ = 0, finished_ = 0;
+  int dev_ = -1;
+  hipError_t result_ = hipSuccess;
+};
+
+}  // namespace
+
 hipError_t quiet(const std::function<hipError_t()> &f) {
   if (hipPeekAtLastError() == hipSuccess) {
     const hipError_t e = f();
@@ -26,13 +86,7 @@ hipError_t quiet(const std::function<hipError_t()> &f) {
     return e;
   }
   // the caller's error is pending: run the call where its error cannot replace the caller's
-  hipError_t e = hipSuccess;
-  std::thread t([&] {
-    e = f();
-    if (e != hipSuccess) (void)hipGetLastError();
-  });
-  t.join();
-  return e;
+  return QuietThread::get().run(f);
 }
 
 namespace eng {
@@ -195,17 +249,6 @@ bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &
   size_t total = 0;
   for (const auto &r : regions) total += static_cast<size_t>(r.second - r.first);
   if (total < min_bytes) return false;  // packing a small batch is cheaper than the syscalls
-  // Never register pages someone has already page-locked: HIP keeps one registration per range,
-  // so registering a caller's registered arena again succeeds and our unregister at the end of
-  // the call then drops the CALLER's registration (its own hipHostUnregister later fails with
-  // hipErrorHostMemoryNotRegistered, and its kernels lose the mapping; round 5,
-  // tools/probes/unregister_probe.py).  Such memory is page-locked already: it packs (or DMAs in
-  // place when caller_pinned recognised it) instead.
-  for (const auto &r : regions)
-    for (const char *q : {static_cast<const char *>(r.first), static_cast<const char *>(r.second - 1)}) {
-      const PtrInfo i = query_ptr(q);
-      if (i.ok && i.type != hipMemoryTypeUnregistered) return false;
-    }
   // Each DMA from registered pageable memory has a fixed cost on top of the bytes, so pin
   // only when the copies the pinned path will issue (one per run of host-contiguous chunks,
   // stripe by stripe) average >= 2.5 MiB; smaller runs pack faster.  Round 1's 4 MiB had
@@ -227,6 +270,18 @@ bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &
   }
   if (runs == 0) return false;
   if (total / runs < min_run) return false;
+  // (after the cheap checks: a query per region end)
+  // Never register pages someone has already page-locked: HIP keeps one registration per range,
+  // so registering a caller's registered arena again succeeds and our unregister at the end of
+  // the call then drops the CALLER's registration (its own hipHostUnregister later fails with
+  // hipErrorHostMemoryNotRegistered, and its kernels lose the mapping; round 5,
+  // tools/probes/unregister_probe.py).  Such memory is page-locked already: it packs (or DMAs in
+  // place when caller_pinned recognised it) instead.
+  for (const auto &r : regions)
+    for (const char *q : {static_cast<const char *>(r.first), static_cast<const char *>(r.second - 1)}) {
+      const PtrInfo i = query_ptr(q);
+      if (i.ok && i.type != hipMemoryTypeUnregistered) return false;
+    }
   {
     // claim the page-rounded regions, so a concurrent call over the same pages packs
     std::lock_guard<std::mutex> lk(g_inplace_mu);

@@ -219,6 +219,16 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   // 2.5 MiB column-block runs per stripe)
   if (pinned && !by_kernel) geometry(std::max(rt.dev_staging_bytes, rt.staging_bytes));
   const size_t slot_bytes = per_col * static_cast<size_t>(cb) * nb_max;
+  // One batch (a lone stripe's call, LStore's per-stripe pattern) has nothing to overlap: its H2D,
+  // kernel and D2H go in order on one stream, so two such calls at once hold two of the process's
+  // hardware queues instead of four (GPU_MAX_HW_QUEUES is 4 on this image, and the stripe server
+  // keeps one).  LSEC_ONE_STREAM=0 keeps the two streams (A/B).
+  static const bool one_stream_ok = [] {
+    const char *e = getenv("LSEC_ONE_STREAM");
+    return !(e && *e == '0');
+  }();
+  const bool one_batch = nb_max >= nstripes && cb >= C;
+  const hipStream_t s_h2d = one_stream_ok && one_batch ? stg->s_out : stg->s_in;
   const auto t_loop0 = now();
   std::vector<DmaRun> runs;
 
@@ -273,14 +283,14 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
                                               reinterpret_cast<uint64_t>(sl.d) + (static_cast<size_t>(s) * nin + j) * len, len)))
               rc = fail("kernel transport: host chunk outside the pinned regions");
         if (rc) break;
-        err = lsec::launch_copy_pieces(sl.pl, static_cast<int>(npin), stg->s_in);
+        err = lsec::launch_copy_pieces(sl.pl, static_cast<int>(npin), s_h2d);
       } else if (pinned) {
         runs.clear();
         for (int s = 0; s < nb; ++s)
           for (int j = 0; j < nin; ++j)
             add_run(runs, sl.d + (static_cast<size_t>(s) * nin + j) * len, ptrs[static_cast<size_t>(s0 + s) * km + in_ids[j]] + c0,
                     len);
-        err = issue_runs(runs, hipMemcpyHostToDevice, stg->s_in);
+        err = issue_runs(runs, hipMemcpyHostToDevice, s_h2d);
       } else {
         jobs.clear();
         for (int s = 0; s < nb; ++s)
@@ -288,10 +298,12 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
             jobs.push_back({sl.h + (static_cast<size_t>(s) * nin + j) * len,
                             ptrs[static_cast<size_t>(s0 + s) * km + in_ids[j]] + c0, len});
         copy_run(jobs);
-        err = hipMemcpyAsync(sl.d, sl.h, in_bytes, hipMemcpyHostToDevice, stg->s_in);
+        err = hipMemcpyAsync(sl.d, sl.h, in_bytes, hipMemcpyHostToDevice, s_h2d);
       }
-      if (err == hipSuccess) err = hipEventRecord(sl.in_done, stg->s_in);
-      if (err == hipSuccess) err = hipStreamWaitEvent(stg->s_out, sl.in_done, 0);
+      if (s_h2d != stg->s_out) {
+        if (err == hipSuccess) err = hipEventRecord(sl.in_done, s_h2d);
+        if (err == hipSuccess) err = hipStreamWaitEvent(stg->s_out, sl.in_done, 0);
+      }
       if (err != hipSuccess) { rc = fail("H2D: %s", hipGetErrorString(err)); break; }
       ShardRef in[kMaxDevs], out[kMaxDevs];
       for (int j = 0; j < nin; ++j)
