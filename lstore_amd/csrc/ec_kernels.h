@@ -103,8 +103,8 @@ struct ApplyArgs {
 // XCD's eighth through an atomic counter, then from the other eighths once its own is done, so
 // the XCDs finish within microseconds of each other.  A slot is kTileQueueWords counters on
 // lines of their own: one per eighth, then a done counter; the launch's last workgroup zeroes
-// them, and slots rotate over a ring per device, so a slot is reused only kTileQueueRing launches
-// later.  LSEC_TILES=static turns it off (A/B).
+// them, and slots rotate over a ring per device; a slot is taken again only after an event
+// recorded behind its last launch has completed.  LSEC_TILES=static turns it off (A/B).
 constexpr int kTileQueueLine = 32;  // unsigned words per counter (a 128-B line each)
 constexpr int kTileQueueWords = 9 * kTileQueueLine;
 constexpr int kTileQueueRing = 4096;
@@ -112,6 +112,9 @@ constexpr int kTileQueueRing = 4096;
 // launch small (fewer than kTileQueueMinTiles), or no slot available (the static eighths serve)
 constexpr uint64_t kTileQueueMinTiles = 16384;
 unsigned *tile_queue_slot(hipStream_t st, uint64_t ntiles);
+// after the launch that took `slot` is queued on st: records the slot's event and frees it for a
+// later taker (who waits for that event first: a slot is never shared by two unfinished launches)
+void tile_queue_release(hipStream_t st, unsigned *slot);
 // with tile sharing on, the tiles of each eighth (of ntiles) dealt statically, one per block,
 // before the sharing blocks take the rest (LSEC_TILES=shared: none; the default keeps 7/8)
 uint32_t tiles_prefix(uint32_t ntiles);

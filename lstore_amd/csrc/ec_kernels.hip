@@ -27,6 +27,11 @@ constexpr int kQueueDevs = 64;
 std::once_flag g_queue_once[kQueueDevs];
 unsigned *g_queue[kQueueDevs];
 std::atomic<uint32_t> g_queue_next[kQueueDevs];
+struct SlotState {
+  std::atomic<int> busy{0};  // taken by a launch that has not recorded its event yet
+  hipEvent_t ev = nullptr;   // recorded after the slot's last launch
+};
+SlotState *g_slots[kQueueDevs];
 int g_cus[kQueueDevs];
 
 // tile mode: 0 static eighths, 1 all tiles shared, 2 a static prefix and a shared tail
@@ -134,11 +139,36 @@ unsigned *tile_queue_slot(hipStream_t st, uint64_t ntiles) {
       return;
     }
     g_cus[dev] = cus;
-    g_queue[dev] = static_cast<unsigned *>(p);  // kept for the process's life
+    g_slots[dev] = new SlotState[kTileQueueRing];  // kept for the process's life, as the queue
+    g_queue[dev] = static_cast<unsigned *>(p);
   });
   if (!g_queue[dev]) return nullptr;
-  const uint32_t i = g_queue_next[dev].fetch_add(1, std::memory_order_relaxed) % kTileQueueRing;
-  return g_queue[dev] + static_cast<size_t>(i) * kTileQueueWords;
+  // a slot no launch still holds: not one between its taking and its event (busy), and not one
+  // whose last launch has yet to finish (its event; normally long done, a ring later)
+  SlotState *slots = g_slots[dev];
+  for (int tries = 0; tries < kTileQueueRing; ++tries) {
+    const uint32_t i = g_queue_next[dev].fetch_add(1, std::memory_order_relaxed) % kTileQueueRing;
+    if (slots[i].busy.exchange(1, std::memory_order_acquire) != 0) continue;
+    if (slots[i].ev && quiet([&] { return hipEventSynchronize(slots[i].ev); }) != hipSuccess) {
+      slots[i].busy.store(0, std::memory_order_release);
+      return nullptr;
+    }
+    return g_queue[dev] + static_cast<size_t>(i) * kTileQueueWords;
+  }
+  return nullptr;
+}
+
+void tile_queue_release(hipStream_t st, unsigned *slot) {
+  if (!slot) return;
+  const int dev = stream_device(st);
+  if (dev < 0 || dev >= kQueueDevs || !g_queue[dev]) return;
+  SlotState &ss = g_slots[dev][(slot - g_queue[dev]) / kTileQueueWords];
+  if (!ss.ev && quiet([&] { return hipEventCreateWithFlags(&ss.ev, hipEventDisableTiming); }) != hipSuccess) ss.ev = nullptr;
+  // (an event that failed to record keeps its earlier state; the slot's launch was queued on st)
+  if (ss.ev && quiet([&] { return hipEventRecord(ss.ev, st); }) != hipSuccess) {
+    (void)quiet([&] { return hipStreamSynchronize(st); });
+  }
+  ss.busy.store(0, std::memory_order_release);
 }
 
 int persistent_grid(const void *kernel, int grid, hipStream_t st) {
@@ -494,19 +524,21 @@ hipError_t launch_hbm_copy(void *dst, const void *src, uint64_t bytes, hipStream
   if (ntiles == 0) return hipSuccess;
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   int grid = default_grid(ntiles);
-  unsigned *q = tile_queue_slot(st, ntiles);
+  unsigned *const slot = tile_queue_slot(st, ntiles);
+  unsigned *q = nullptr;
   uint32_t pre = 0;
-  if (q) {
+  if (slot) {
     const int pg = persistent_grid(reinterpret_cast<const void *>(&k_hbm_copy), grid, st);
     if (pg > 0) {
+      q = slot;
       pre = tiles_prefix(static_cast<uint32_t>(grid));
       grid = static_cast<int>(8 * pre) + pg;
-    } else {
-      q = nullptr;
     }
   }
-  return launch_kernel(&k_hbm_copy, dim3(grid), dim3(kBlock), st, reinterpret_cast<uint64_t>(dst),
-                     reinterpret_cast<uint64_t>(src), n16, q, pre);
+  const hipError_t e = launch_kernel(&k_hbm_copy, dim3(grid), dim3(kBlock), st, reinterpret_cast<uint64_t>(dst),
+                                     reinterpret_cast<uint64_t>(src), n16, q, pre);
+  tile_queue_release(st, slot);
+  return e;
 }
 
 hipError_t launch_hbm_mix(const ApplyArgs &a, hipStream_t st) {

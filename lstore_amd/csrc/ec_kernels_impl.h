@@ -154,7 +154,7 @@ __device__ __forceinline__ void for_tiles(uint32_t ntiles, unsigned *q, uint32_t
     body(t);
     t += step;
   }
-  // the launch's last sharing block leaves the slot zeroed for its next use (kTileQueueRing launches on)
+  // the launch's last sharing block leaves the slot zeroed for its next taker
   if (sharing && threadIdx.x == 0 && atomicAdd(q + kTileQueueLine * 8, 1u) == gridDim.x - 8 * pre - 1)
     for (int e = 0; e <= 8; ++e) atomicExch(q + kTileQueueLine * e, 0u);
 }
@@ -164,19 +164,21 @@ __device__ __forceinline__ void for_tiles(uint32_t ntiles, unsigned *q, uint32_t
 template <typename Kern>
 hipError_t launch_tiled(Kern *k, int grid, hipStream_t st, ApplyArgs a) {
   a.stamps = launch_stamps(&a.nstamps);
-  a.tiles = tile_queue_slot(st, static_cast<uint64_t>(grid));
+  unsigned *slot = tile_queue_slot(st, static_cast<uint64_t>(grid));
+  a.tiles = nullptr;
   a.tiles_pre = 0;
-  if (a.tiles) {
+  if (slot) {
     const int pg = persistent_grid(reinterpret_cast<const void *>(k), grid, st);
     if (pg > 0) {
       // `grid` is the tile count here (one tile per block in the static form)
+      a.tiles = slot;
       a.tiles_pre = tiles_prefix(static_cast<uint32_t>(grid));
       grid = static_cast<int>(8 * a.tiles_pre) + pg;
-    } else {
-      a.tiles = nullptr;
     }
   }
-  return launch_kernel(k, dim3(grid), dim3(kBlock), st, a);
+  const hipError_t e = launch_kernel(k, dim3(grid), dim3(kBlock), st, a);
+  tile_queue_release(st, slot);
+  return e;
 }
 
 // ------------------------------------------------------------------ adler32 partial sums

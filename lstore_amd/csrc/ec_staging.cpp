@@ -34,7 +34,8 @@ struct Staging {
   struct Slot {
     char *d = nullptr;   // device: [nb][nin][C] then [nb][nout][C]
     char *h = nullptr;   // pinned host, same layout
-    size_t cap = 0;
+    size_t cap = 0;      // bytes at d
+    size_t hcap = 0;     // bytes at h (grown on its own: see ensure_slot)
     hipEvent_t in_done = nullptr, done = nullptr;
     bool pending = false;
     // what to unpack when `done` fires
@@ -96,18 +97,26 @@ void release_staging(Staging *s) {
 // Slots are sized for a full batch (half the staging budget) the first time, so that a
 // small first call does not leave them too small for the next one: re-pinning 64 MiB of
 // host memory costs more than moving it over PCIe.  need_host = false (pinned callers, see
-// below) allocates only the device half.
+// below) needs only the device half.  The two halves grow independently: a pinned caller's
+// larger device geometry (dev_staging_bytes) must not free the host half a packed caller
+// will want again, or alternating pinned encodes and packed decodes re-pin the host half on
+// every call (a 2x host-path loss the round-5 c5 sweep showed).
 int ensure_slot(Staging::Slot &sl, size_t bytes, bool need_host = true) {
-  if (sl.cap >= bytes && (sl.h || !need_host)) return 0;
-  if (sl.d) (void)hipFree(sl.d);
-  if (sl.h) (void)hipHostFree(sl.h);
-  sl.d = nullptr;
-  sl.h = nullptr;
-  sl.cap = 0;
   const size_t cap = std::max(bytes, routes().staging_bytes / 2);
-  HIP_OK(hipMalloc(&sl.d, cap));
-  if (need_host) HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&sl.h), cap, hipHostMallocDefault));
-  sl.cap = cap;
+  if (sl.cap < bytes) {
+    if (sl.d) (void)hipFree(sl.d);
+    sl.d = nullptr;
+    sl.cap = 0;
+    HIP_OK(hipMalloc(&sl.d, cap));
+    sl.cap = cap;
+  }
+  if (need_host && sl.hcap < bytes) {
+    if (sl.h) (void)hipHostFree(sl.h);
+    sl.h = nullptr;
+    sl.hcap = 0;
+    HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&sl.h), cap, hipHostMallocDefault));
+    sl.hcap = cap;
+  }
   return 0;
 }
 
@@ -222,10 +231,12 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   // One batch (a lone stripe's call, LStore's per-stripe pattern) has nothing to overlap: its H2D,
   // kernel and D2H go in order on one stream, so two such calls at once hold two of the process's
   // hardware queues instead of four (GPU_MAX_HW_QUEUES is 4 on this image, and the stripe server
-  // keeps one).  LSEC_ONE_STREAM=0 keeps the two streams (A/B).
+  // keeps one).  Measured level with two streams on LStore's 1 MiB per-stripe decodes (1 thread
+  // 32.6 vs 30.5 GiB/s, 2 threads 35.0 vs 36.3, inside the reference's own run-to-run spread;
+  // profiles/r05_v8_fnptr_one_stream.jsonl), so it stays an option: LSEC_ONE_STREAM=1.
   static const bool one_stream_ok = [] {
     const char *e = getenv("LSEC_ONE_STREAM");
-    return !(e && *e == '0');
+    return e && *e == '1';
   }();
   const bool one_batch = nb_max >= nstripes && cb >= C;
   const hipStream_t s_h2d = one_stream_ok && one_batch ? stg->s_out : stg->s_in;
