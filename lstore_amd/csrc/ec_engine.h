@@ -158,7 +158,8 @@ struct RouteTable {
   // transports
   bool pin_in_place;           // LSEC_NO_HOST_REGISTER unset: pageable batches may be pinned in place for DMA
   size_t pin_min_bytes;        // LSEC_PIN_MIN_KB = 8192: ... when the batch has at least this many bytes
-  size_t pin_min_run;          // LSEC_PIN_MIN_RUN_KB = 2560: ... and its DMA copies average this run
+  size_t pin_min_run;          // LSEC_PIN_MIN_RUN_KB = 6144: ... and its DMA copies average this run
+                               //   (waived for one-region batches of >= 4 stripes: strided copies)
   bool kernel_copy;            // LSEC_KERNEL_COPY != 0: hipHostMalloc'd caller runs may move by kernel
   size_t kernel_copy_max_run;  // 1 MiB: ... when their runs average less
   int slot_pack_pool;          // LSEC_ZC_POOL: -1 (default) own-slot calls pack on the pool when

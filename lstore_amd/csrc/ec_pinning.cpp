@@ -8,6 +8,8 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdarg>
+#include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -251,13 +253,12 @@ bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &
   if (total < min_bytes) return false;  // packing a small batch is cheaper than the syscalls
   // Each DMA from registered pageable memory has a fixed cost on top of the bytes, so pin
   // only when the copies the pinned path will issue (one per run of host-contiguous chunks,
-  // stripe by stripe) average >= 2.5 MiB; smaller runs pack faster.  Round 1's 4 MiB had
-  // every single-erasure decode below C = 2 MiB packing (RS(6+3) 1 MiB decode: 3.5 MiB runs,
-  // 31 GiB/s packed, 37-46 pinned).  An in-process A/B (tools/pin_run_ab.py,
-  // profiles/r02_v27_pin_run_ab.jsonl) put the break-even near 800 KiB, but the c5 sweep
-  // with that threshold (r02_v38_sweep_c5.jsonl vs r02_v25) lost up to half the rate at
-  // 1.5-2.25 MiB runs (RS(6+3) 256 KiB encode 32 -> 16, 512 KiB 29 -> 22.5) while runs of
-  // 2.75 MiB and up gained (RS(10+4) 512 KiB decode 30 -> 40).
+  // stripe by stripe) average >= pin_min_run; smaller runs pack faster.  History: round 1's
+  // 4 MiB; 2.5 MiB from round 2 (profiles/r02_v38_sweep_c5.jsonl vs r02_v25: 800 KiB lost half
+  // the rate at 1.5-2.25 MiB runs); 6 MiB from round 5, once one-region batches moved to strided
+  // copies: the remaining per-run decodes at 2.5-4.5 MiB runs reached 0.76-0.87 of the link
+  // pinned against 0.91-0.93 packed (RS(4+2) 1 MiB 0.769 -> 0.906, RS(6+3) 1 MiB 0.837 -> 0.913;
+  // profiles/r05_v10_dma2d_ab.jsonl).
   size_t runs = 0;
   for (const std::vector<int> *ids : {&in_ids, &out_ids}) {
     const char *end = nullptr;
@@ -269,7 +270,12 @@ bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &
       }
   }
   if (runs == 0) return false;
-  if (total / runs < min_run) return false;
+  // One region (an encode over [stripe][k+m][C] batches: every chunk moves) is one registration,
+  // and its runs repeat at one stride, so they go as strided copies (issue_runs) whatever their
+  // length: the per-copy cost the threshold prices is gone.  Several regions (a decode's
+  // survivors with the unused parity between stripes) keep one copy per run.
+  // (A lone stripe or two have no stride to share: they keep the threshold.)
+  if ((regions.size() > 1 || nstripes < 4) && total / runs < min_run) return false;
   // (after the cheap checks: a query per region end)
   // Never register pages someone has already page-locked: HIP keeps one registration per range,
   // so registering a caller's registered arena again succeeds and our unregister at the end of
@@ -399,10 +405,94 @@ void split_pieces(std::vector<lsec::CopyPiece> &v, uint64_t src, uint64_t dst, s
   for (size_t o = 0; o < len; o += lsec::kPieceBytes) v.push_back({src + o, dst + o, std::min<uint64_t>(lsec::kPieceBytes, len - o)});
 }
 
+// Runs that repeat with one stripe stride on both sides (the p chunks a stripe moves, stripe after
+// stripe: p = 1 for encode's k data chunks, 2 for a decode whose erasure splits the survivors) go
+// as p strided copies (hipMemcpy2DAsync, one row per stripe) instead of one copy per run: per-copy
+// gaps hold one copy per 4 MiB run to 49.5 GB/s of the link's 57.6 H2D, and 1-2 MiB D2H runs to
+// 10-45 GB/s, where the strided copy runs at 57.6 / 57.0 (profiles/r05_v10_rect_probe.jsonl).
+// LSEC_DMA_2D=0 issues one copy per run.
+namespace {
+struct Lattice {
+  size_t period = 0, rows = 0;
+  ptrdiff_t sp = 0, dp = 0;
+};
+
+// the longest lattice starting at v[i]: `period` runs repeated `rows` times at strides sp / dp
+Lattice lattice_at(const std::vector<DmaRun> &v, size_t i) {
+  Lattice best;
+  const size_t n = v.size();
+  for (size_t p = 1; p <= 8 && i + p < n; ++p) {
+    const ptrdiff_t sp = v[i + p].src - v[i].src, dp = v[i + p].dst - v[i].dst;
+    if (sp <= 0 || dp <= 0) continue;
+    bool fits = true;  // every lane's row fits its pitch
+    for (size_t l = 0; l < p && fits; ++l) fits = static_cast<size_t>(sp) >= v[i + l].bytes && static_cast<size_t>(dp) >= v[i + l].bytes;
+    if (!fits) continue;
+    size_t rows = 1;
+    for (;; ++rows) {
+      const size_t b = i + rows * p;
+      if (b + p > n) break;
+      bool same = true;
+      for (size_t l = 0; l < p && same; ++l)
+        same = v[b + l].bytes == v[i + l].bytes && v[b + l].src - v[b + l - p].src == sp && v[b + l].dst - v[b + l - p].dst == dp;
+      if (!same) break;
+    }
+    if (rows >= 2 && rows * p > best.rows * best.period) best = {p, rows, sp, dp};
+  }
+  return best;
+}
+
+// [p, p + span) inside one allocation or registered range: a strided copy is validated against
+// the allocation holding its first byte, and in-place pinning registers only the chunks a call
+// moves, so a lattice over a decode's survivors can step over unregistered chunks
+// (hipMemcpy2DAsync: invalid argument)
+bool one_range(const char *p, size_t span) {
+  void *start = nullptr;
+  size_t size = 0;
+  const hipDeviceptr_t d = reinterpret_cast<hipDeviceptr_t>(const_cast<char *>(p));
+  if (quiet([&] {
+        const hipError_t r = hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, d);
+        return r != hipSuccess ? r : hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, d);
+      }) != hipSuccess)
+    return false;
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(start), u = reinterpret_cast<uintptr_t>(p);
+  return u >= lo && u + span <= lo + size;
+}
+
+bool lattice_in_ranges(const std::vector<DmaRun> &v, size_t i, const Lattice &g) {
+  size_t lo_s = SIZE_MAX, hi_s = 0, lo_d = SIZE_MAX, hi_d = 0;
+  for (size_t l = 0; l < g.period; ++l) {
+    const DmaRun &a = v[i + l], &b = v[i + (g.rows - 1) * g.period + l];
+    lo_s = std::min(lo_s, reinterpret_cast<size_t>(a.src));
+    hi_s = std::max(hi_s, reinterpret_cast<size_t>(b.src) + b.bytes);
+    lo_d = std::min(lo_d, reinterpret_cast<size_t>(a.dst));
+    hi_d = std::max(hi_d, reinterpret_cast<size_t>(b.dst) + b.bytes);
+  }
+  return one_range(reinterpret_cast<const char *>(lo_s), hi_s - lo_s) &&
+         one_range(reinterpret_cast<const char *>(lo_d), hi_d - lo_d);
+}
+}  // namespace
+
 hipError_t issue_runs(const std::vector<DmaRun> &v, hipMemcpyKind kind, hipStream_t st) {
-  for (const DmaRun &r : v) {
-    const hipError_t e = hipMemcpyAsync(r.dst, r.src, r.bytes, kind, st);
-    if (e != hipSuccess) return e;
+  static const bool strided = [] {
+    const char *e = getenv("LSEC_DMA_2D");
+    return !(e && *e == '0');
+  }();
+  for (size_t i = 0; i < v.size();) {
+    const Lattice g = strided ? lattice_at(v, i) : Lattice{};
+    const size_t end = g.rows >= 2 ? i + g.period * g.rows : i + 1;
+    if (g.rows >= 2 && lattice_in_ranges(v, i, g)) {
+      for (size_t l = 0; l < g.period; ++l) {
+        const DmaRun &r = v[i + l];
+        const hipError_t e = hipMemcpy2DAsync(r.dst, static_cast<size_t>(g.dp), r.src, static_cast<size_t>(g.sp), r.bytes, g.rows, kind, st);
+        if (e != hipSuccess) return e;
+      }
+    } else {  // (a lattice over more than one range: its runs one by one)
+      for (size_t j = i; j < end; ++j) {
+        const hipError_t e = hipMemcpyAsync(v[j].dst, v[j].src, v[j].bytes, kind, st);
+        if (e != hipSuccess) return e;
+      }
+    }
+    i = end;
   }
   return hipSuccess;
 }

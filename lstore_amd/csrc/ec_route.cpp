@@ -47,7 +47,7 @@ const RouteTable &routes() {
     r.srv_early_out = env("LSEC_SRV_EARLY_OUT", 1) != 0;
     r.pin_in_place = getenv("LSEC_NO_HOST_REGISTER") == nullptr;
     r.pin_min_bytes = static_cast<size_t>(std::max(0L, env("LSEC_PIN_MIN_KB", 8192))) << 10;
-    r.pin_min_run = static_cast<size_t>(std::max(0L, env("LSEC_PIN_MIN_RUN_KB", 2560))) << 10;
+    r.pin_min_run = static_cast<size_t>(std::max(0L, env("LSEC_PIN_MIN_RUN_KB", 6144))) << 10;
     r.kernel_copy = env("LSEC_KERNEL_COPY", 1) != 0;
     r.kernel_copy_max_run = 1u << 20;
     r.slot_pack_pool = static_cast<int>(env("LSEC_ZC_POOL", -1));

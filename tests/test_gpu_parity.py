@@ -778,6 +778,44 @@ def test_host_path_pinned_buffers(cuda, method, k, m, size, n):
         assert np.array_equal(st[:, [1, k + 1]], keep)
 
 
+@pytest.mark.parametrize("method", [L.REED_SOL_VAN, L.CAUCHY_GOOD])
+def test_strided_dma_lattices(cuda, method):
+    """Pinned-DMA batches go as strided copies when their runs repeat at one stripe stride
+    (issue_runs, ec_pinning.cpp): one lane (encode's data chunks), several lanes (erasures that
+    split the survivors into runs of different lengths), and pointer arrays whose stripes do NOT
+    sit at one stride (two allocations, stripes in shuffled order) -- every result equal to the
+    oracle's."""
+    k, m, size, n = 8, 4, 4 << 20, 6  # 4 MiB chunks: runs well above the in-place pinning thresholds
+    rng = np.random.default_rng(11)
+    st = np.zeros((n, k + m, size), np.uint8)
+    st[:, :k] = rng.integers(0, 256, (n, k, size), dtype=np.uint8)
+    with L.Plan.for_chunk(method, k, m, size) as p:
+        p.encode_stripes(st)
+        for s in (0, n - 1):
+            assert np.array_equal(st[s, k:], O.encode(method, st[s, :k], m, p.packet_size)), s
+        full = st.copy()
+        for erased in ([2, 5, 9], [0, 3, 6, 11], [1, 8]):
+            st[:, erased] = 0x3C
+            p.decode_stripes(st, erased)
+            assert np.array_equal(st, full), erased
+        # stripes from two allocations, in shuffled order: no single stride
+        a = full[: n // 2].copy()
+        b = full[n // 2:].copy()
+        order = [3, 0, 5, 1, 4, 2]
+        rows = [(a if i < n // 2 else b)[i % (n // 2)] for i in order]
+        for r in rows:
+            r[k:] = 0
+        addrs = [r[i].ctypes.data for r in rows for i in range(k + m)]
+        p.encode_stripes_ptrs(p._ptr_array(addrs), n, size)
+        for r, i in zip(rows, order):
+            assert np.array_equal(r, full[i]), i
+        for r in rows:
+            r[[1, 2, k]] = 0
+        p.decode_stripes_ptrs(p._ptr_array(addrs), n, size, [1, 2, k])
+        for r, i in zip(rows, order):
+            assert np.array_equal(r, full[i]), i
+
+
 def test_pageable_batches_pinned_in_place_share_inputs(cuda):
     """Large pageable batches are pinned in place (hipHostRegister) for the call.  Threads that
     encode from the SAME data chunks at once (each into its own parity buffers) contend for

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--pattern", default="EEEDDDEDEDED")
     ap.add_argument("--dev-first", action="store_true")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--keep-cache", action="store_true", help="free the device phase's tensors to torch's cache only")
+    ap.add_argument("--sleep", type=float, default=0.0, help="seconds to wait after the device phase")
     a = ap.parse_args()
     k, m = (int(x) for x in a.km.split("+"))
     C = a.chunk
@@ -43,7 +45,9 @@ def main():
         p.encode_dev(d, par)
         torch.cuda.synchronize()
         del d, par
-        torch.cuda.empty_cache()
+        if not a.keep_cache:
+            torch.cuda.empty_cache()
+        time.sleep(a.sleep)
     n = max(2, (1 << 30) // (k * C))
     buf = np.empty((n, k + m, C), dtype=np.uint8)
     buf[:] = np.random.default_rng(1).integers(0, 256, (1, k + m, C), dtype=np.uint8)
@@ -55,7 +59,7 @@ def main():
         else:
             p.decode_stripes(buf, [0])
         t = time.perf_counter() - t0
-        print(json.dumps({"tag": a.tag, "km": a.km, "chunk": C, "dev_first": a.dev_first, "i": i, "op": op,
+        print(json.dumps({"tag": a.tag, "km": a.km, "chunk": C, "dev_first": a.dev_first, "keep_cache": a.keep_cache, "sleep": a.sleep, "i": i, "op": op,
                           "ms": round(t * 1e3, 2), "user_gibps": round(k * C * n / t / 2**30, 2)}), flush=True)
 
 

@@ -106,14 +106,20 @@ def main():
                 ok &= bool(torch.equal(rb[:, 0], data[:, 0]))
                 del data, par, rb
                 torch.cuda.empty_cache()
-                # host path with copies included
+                # host path with copies included.  The device phase just handed ~12 GiB back to the
+                # driver; for ~0.2 s after such a free, host<->device DMA runs at 60-70 % of its rate
+                # (profiles/r05_v9_host_pattern.jsonl: a 2 s pause, or keeping the memory in torch's
+                # cache, removes it), so pause, and warm the host batch with one untimed pair.
+                torch.cuda.synchronize()
+                time.sleep(1.0)
                 Nh = max(2, int(a.host_gib * 2**30 / (k * C)))
                 buf = np.empty((Nh, k + m, C), dtype=np.uint8)
                 tile = np.random.default_rng(k * 31 + m).integers(0, 256, (1, k + m, C), dtype=np.uint8)
                 buf[:] = tile
-                plan.encode_stripes(buf[:1])
+                plan.encode_stripes(buf)
+                plan.decode_stripes(buf, [0])
                 tes, tds = [], []
-                for _ in range(a.reps):  # median of reps: the first call on a fresh buffer varies
+                for _ in range(a.reps):  # median of reps
                     t0 = time.perf_counter()
                     plan.encode_stripes(buf)
                     tes.append(time.perf_counter() - t0)
