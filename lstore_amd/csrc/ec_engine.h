@@ -151,6 +151,8 @@ struct RouteTable {
                                // takes route 4 pinned in place (DMA, no packing) ...
   size_t own_dma_min_bytes;    // 1 MiB: ... when the call has this many bytes ...
   size_t own_dma_min_run;      // LSEC_OWN_DMA_MIN_RUN_KB = 1024: ... and its DMA runs average this
+  int lone_blocks;             // LSEC_LONE_BLOCKS = 1: a lone stripe DMA'd in place moves in this many
+                               // column blocks (block b+1's H2D under block b's kernel and D2H)
   bool server;                 // LSEC_SERVER = 1: route 1 on
   size_t srv_nt_min;           // LSEC_SRV_NT_MIN_KB (off): server calls copying this much in use streaming stores
   bool srv_early_out;          // LSEC_SRV_EARLY_OUT = 1: a spinning server caller copies each part's

@@ -227,6 +227,14 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   // device budget, and wide stripes move whole (RS(20+6) at 4 MiB: 80 MiB runs instead of twenty
   // 2.5 MiB column-block runs per stripe)
   if (pinned && !by_kernel) geometry(std::max(rt.dev_staging_bytes, rt.staging_bytes));
+  // A lone stripe DMA'd in place (LStore's per-stripe calls on route 4) in column blocks: each
+  // block's chunks repeat at the chunk stride, so a block moves as one strided copy each way
+  // (issue_runs), and block b+1's H2D runs under block b's kernel and D2H
+  if (pinned && !by_kernel && nstripes == 1 && rt.lone_blocks > 1 && cb == C) {
+    const long long align = packet_kind(kind) ? static_cast<long long>(p->w) * p->packet_size : 8192;
+    const long long b = (C / rt.lone_blocks + align - 1) / align * align;
+    if (b < C) cb = b;
+  }
   const size_t slot_bytes = per_col * static_cast<size_t>(cb) * nb_max;
   // One batch (a lone stripe's call, LStore's per-stripe pattern) has nothing to overlap: its H2D,
   // kernel and D2H go in order on one stream, so two such calls at once hold two of the process's
