@@ -411,7 +411,6 @@ void split_pieces(std::vector<lsec::CopyPiece> &v, uint64_t src, uint64_t dst, s
 // gaps hold one copy per 4 MiB run to 49.5 GB/s of the link's 57.6 H2D, and 1-2 MiB D2H runs to
 // 10-45 GB/s, where the strided copy runs at 57.6 / 57.0 (profiles/r05_v10_rect_probe.jsonl).
 // LSEC_DMA_2D=0 issues one copy per run.
-namespace {
 struct Lattice {
   size_t period = 0, rows = 0;
   ptrdiff_t sp = 0, dp = 0;
@@ -441,6 +440,7 @@ Lattice lattice_at(const std::vector<DmaRun> &v, size_t i) {
   return best;
 }
 
+namespace {
 // [p, p + span) inside one allocation or registered range: a strided copy is validated against
 // the allocation holding its first byte, and in-place pinning registers only the chunks a call
 // moves, so a lattice over a decode's survivors can step over unregistered chunks
@@ -499,3 +499,28 @@ hipError_t issue_runs(const std::vector<DmaRun> &v, hipMemcpyKind kind, hipStrea
 
 }  // namespace eng
 }  // namespace lsec
+
+// Test hook, not part of include/*.h: how issue_runs would group n DMA runs (dst[i], src[i],
+// bytes[i], in issue order) into strided lattices, before the registered-range check (which needs
+// the runtime).  Writes (first run, period, rows, src pitch, dst pitch) per group to out; a lone
+// run is period 1, rows 1.  Returns the number of groups, or -1 when out_cap is too small.
+extern "C" int lsec_test_lattices(const uint64_t *dst, const uint64_t *src, const uint64_t *bytes, int n, int64_t *out,
+                                  int out_cap) {
+  std::vector<lsec::eng::DmaRun> v;
+  for (int i = 0; i < n; ++i)
+    v.push_back({reinterpret_cast<char *>(dst[i]), reinterpret_cast<const char *>(src[i]), static_cast<size_t>(bytes[i])});
+  int groups = 0;
+  for (size_t i = 0; i < v.size();) {
+    const lsec::eng::Lattice g = lsec::eng::lattice_at(v, i);
+    const bool lat = g.rows >= 2;
+    if (groups >= out_cap) return -1;
+    int64_t *o = out + 5 * groups++;
+    o[0] = static_cast<int64_t>(i);
+    o[1] = lat ? static_cast<int64_t>(g.period) : 1;
+    o[2] = lat ? static_cast<int64_t>(g.rows) : 1;
+    o[3] = lat ? g.sp : 0;
+    o[4] = lat ? g.dp : 0;
+    i += lat ? g.period * g.rows : 1;
+  }
+  return groups;
+}
