@@ -816,6 +816,35 @@ def test_strided_dma_lattices(cuda, method):
             assert np.array_equal(r, full[i]), i
 
 
+@pytest.mark.parametrize("method,k,m,size,n,w", [
+    (L.REED_SOL_VAN, 8, 3, 512 << 10, 24, 8), (L.REED_SOL_VAN, 4, 2, 1 << 20, 16, 8),
+    (L.REED_SOL_VAN, 16, 4, 256 << 10, 32, 8), (L.CAUCHY_GOOD, 6, 3, 1 << 20, 12, 8),
+    (L.CAUCHY_GOOD, 10, 4, 2 << 20, 6, 8), (L.REED_SOL_VAN, 6, 3, 1 << 20, 12, 16),
+    (L.CAUCHY_GOOD, 8, 4, 1 << 20, 8, 32)])
+def test_host_batches_match_device_path(cuda, method, k, m, size, n, w):
+    """Every stripe of a pageable host batch (pinned in place, strided copies; or packed) equals
+    the device-resident path's result byte for byte, for encode and for decodes whose erasures
+    split the survivors into one, two and three runs per stripe."""
+    import torch
+
+    rng = np.random.default_rng(k * 100 + m + w)
+    st = np.zeros((n, k + m, size), np.uint8)
+    st[:, :k] = rng.integers(0, 256, (n, k, size), dtype=np.uint8)
+    with L.Plan.for_chunk(method, k, m, size, w=w) as p:
+        d = torch.from_numpy(st[:, :k].copy()).cuda()
+        par = torch.empty((n, m, size), dtype=torch.uint8, device="cuda")
+        p.encode_dev(d, par)
+        p.encode_stripes(st)
+        torch.cuda.synchronize()
+        assert np.array_equal(st[:, k:], par.cpu().numpy())
+        full = st.copy()
+        for erased in ([0], [1, k], [2, 5 % k, k + m - 1]):
+            erased = sorted(set(erased))[:m]
+            st[:, erased] = 0x96
+            p.decode_stripes(st, erased)
+            assert np.array_equal(st, full), erased
+
+
 def test_pageable_batches_pinned_in_place_share_inputs(cuda):
     """Large pageable batches are pinned in place (hipHostRegister) for the call.  Threads that
     encode from the SAME data chunks at once (each into its own parity buffers) contend for
