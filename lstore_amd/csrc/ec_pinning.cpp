@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -321,19 +322,88 @@ bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &
   return true;
 }
 
-void InPlacePin::release() {
-  for (char *b : held_)
+namespace {
+void unregister_all(const std::vector<char *> &held) {
+  for (char *b : held)
     if (quiet([&] { return hipHostUnregister(b); }) != hipSuccess) {
       static std::atomic<bool> told{false};
       if (!told.exchange(true)) fprintf(stderr, "liblstore_ec: hipHostUnregister(%p) failed\n", static_cast<void *>(b));
     }
-  held_.clear();
-  if (claimed_.empty()) return;
+}
+
+void unclaim(const std::vector<std::pair<uintptr_t, uintptr_t>> &claimed) {
+  if (claimed.empty()) return;
   std::lock_guard<std::mutex> lk(g_inplace_mu);
-  for (const auto &c : claimed_) {
+  for (const auto &c : claimed) {
     auto it = std::find(g_inplace.begin(), g_inplace.end(), c);
     if (it != g_inplace.end()) g_inplace.erase(it);
   }
+}
+
+// hipHostUnregister waits until every queue of the device is idle (tools/probes/
+// unregister_wait_probe.cpp: 4.5 ms behind another thread's 256 MiB copy, and no progress at all
+// while that thread re-submits after each hipStreamSynchronize), so two callers' registrations
+// released at the ends of their calls march in lockstep.  With LSEC_DEFER_UNPIN_MB the release
+// goes to this thread instead: the ranges stay claimed (no other call takes or re-registers them)
+// until they are unregistered, and a caller whose release would put more than the cap in flight
+// waits for the backlog.  Leaked singleton: registrations still pending at exit go with the process.
+class Unpinner {
+ public:
+  static Unpinner &get() {
+    static Unpinner *u = new Unpinner();
+    return *u;
+  }
+  void put(std::vector<char *> held, std::vector<std::pair<uintptr_t, uintptr_t>> claimed, size_t bytes, size_t cap) {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return pending_ == 0 || pending_ + bytes <= cap; });
+    q_.push_back({std::move(held), std::move(claimed), bytes});
+    pending_ += bytes;
+    work_.notify_one();
+  }
+
+ private:
+  struct Item {
+    std::vector<char *> held;
+    std::vector<std::pair<uintptr_t, uintptr_t>> claimed;
+    size_t bytes;
+  };
+  Unpinner() { std::thread([this] { loop(); }).detach(); }
+  void loop() {
+    for (;;) {
+      Item it;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        work_.wait(lk, [&] { return !q_.empty(); });
+        it = std::move(q_.front());
+        q_.pop_front();
+      }
+      unregister_all(it.held);
+      unclaim(it.claimed);
+      std::lock_guard<std::mutex> lk(mu_);
+      pending_ -= it.bytes;
+      done_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable work_, done_;
+  std::deque<Item> q_;
+  size_t pending_ = 0;
+};
+}  // namespace
+
+void InPlacePin::release() {
+  const size_t cap = routes().defer_unpin_bytes;
+  if (cap > 0 && !held_.empty()) {
+    size_t bytes = 0;
+    for (const auto &c : claimed_) bytes += c.second - c.first;
+    Unpinner::get().put(std::move(held_), std::move(claimed_), bytes, cap);
+    held_.clear();
+    claimed_.clear();
+    return;
+  }
+  unregister_all(held_);
+  held_.clear();
+  unclaim(claimed_);
   claimed_.clear();
 }
 
