@@ -262,6 +262,13 @@ void lsec_set_kernel_variant(int bytewise_variant, int bitsliced_variant);  /* t
  * mode. */
 void lsec_set_tile_sharing(int mode);
 int lsec_tile_sharing(void);
+/* Pageable host chunks a call pins in place (hipHostRegister) are unregistered when the call ends;
+ * while other calls hold registrations of their own, a background thread does it instead, shortly
+ * after the call returns (hipHostUnregister waits until the whole device is idle, so calls on
+ * several threads would otherwise wait for each other's transfers; LSEC_DEFER_UNPIN_MB caps what
+ * may be pending, 0 turns it off).  A caller that registers host memory with HIP itself, or hands
+ * such memory to another HIP user, calls this first: it returns when nothing is pending.  0. */
+int lsec_host_unpin_drain(void);
 /* Measurement probe, not part of the coding path: enqueue a streaming device copy dst <- src
  * (bytes a multiple of 16, 16-byte aligned device pointers) on `stream` with the coding kernels'
  * memory shape; bench.py times it as the box's practical HBM ceiling.  0 / -1. */

@@ -129,6 +129,7 @@ bool is_pinned_host(const void *ptr) {
 // it returns, maybe while the other call's DMA is still queued.
 std::mutex g_inplace_mu;
 std::vector<std::pair<uintptr_t, uintptr_t>> g_inplace;
+std::atomic<int> g_pins_held{0};  // calls holding in-place registrations right now (InPlacePin)
 
 bool inplace_overlaps_locked(uintptr_t lo, uintptr_t hi) {
   for (const auto &r : g_inplace)
@@ -314,11 +315,13 @@ bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &
     char *hi = reinterpret_cast<char *>((reinterpret_cast<uintptr_t>(r.second) + kPage - 1) & ~(kPage - 1));
     if (quiet([&] { return hipHostRegister(lo, static_cast<size_t>(hi - lo), hipHostRegisterPortable | hipHostRegisterMapped); }) !=
         hipSuccess) {
+      g_pins_held.fetch_add(1, std::memory_order_acq_rel);  // (release() counts this call out)
       release();
       return false;
     }
     held_.push_back(lo);
   }
+  g_pins_held.fetch_add(1, std::memory_order_acq_rel);
   return true;
 }
 
@@ -352,6 +355,11 @@ class Unpinner {
   static Unpinner &get() {
     static Unpinner *u = new Unpinner();
     return *u;
+  }
+  // until nothing is pending (lsec_host_unpin_drain)
+  void drain() {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return pending_ == 0 && q_.empty(); });
   }
   void put(std::vector<char *> held, std::vector<std::pair<uintptr_t, uintptr_t>> claimed, size_t bytes, size_t cap) {
     std::unique_lock<std::mutex> lk(mu_);
@@ -391,9 +399,16 @@ class Unpinner {
 };
 }  // namespace
 
+Unpinner *g_unpinner = nullptr;  // set once the first deferred release made it
+
 void InPlacePin::release() {
+  if (held_.empty() && claimed_.empty()) return;
+  const bool others = g_pins_held.fetch_sub(1, std::memory_order_acq_rel) > 1;
   const size_t cap = routes().defer_unpin_bytes;
-  if (cap > 0 && !held_.empty()) {
+  // deferred only while another call is in flight: alone, the unregister is immediate (the runtime
+  // re-registers recently registered pages in microseconds, and nothing else of ours is running)
+  if (cap > 0 && others && !held_.empty()) {
+    g_unpinner = &Unpinner::get();
     size_t bytes = 0;
     for (const auto &c : claimed_) bytes += c.second - c.first;
     Unpinner::get().put(std::move(held_), std::move(claimed_), bytes, cap);
@@ -574,6 +589,13 @@ hipError_t issue_runs(const std::vector<DmaRun> &v, hipMemcpyKind kind, hipStrea
 // bytes[i], in issue order) into strided lattices, before the registered-range check (which needs
 // the runtime).  Writes (first run, period, rows, src pitch, dst pitch) per group to out; a lone
 // run is period 1, rows 1.  Returns the number of groups, or -1 when out_cap is too small.
+// include/lstore_ec.h: wait until every in-place registration a call left to the background
+// unpinner is dropped (before the caller registers host memory with HIP itself)
+extern "C" int lsec_host_unpin_drain(void) {
+  if (lsec::eng::g_unpinner) lsec::eng::g_unpinner->drain();
+  return 0;
+}
+
 extern "C" int lsec_test_lattices(const uint64_t *dst, const uint64_t *src, const uint64_t *bytes, int n, int64_t *out,
                                   int out_cap) {
   std::vector<lsec::eng::DmaRun> v;

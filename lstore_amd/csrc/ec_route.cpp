@@ -42,7 +42,7 @@ const RouteTable &routes() {
     r.own_dma_max = static_cast<int>(std::max(0L, env("LSEC_OWN_DMA_MAX", 2)));
     r.own_dma_min_bytes = 1u << 20;
     r.own_dma_min_run = static_cast<size_t>(std::max(0L, env("LSEC_OWN_DMA_MIN_RUN_KB", 1024))) << 10;
-    r.defer_unpin_bytes = static_cast<size_t>(std::max(0L, env("LSEC_DEFER_UNPIN_MB", 0))) << 20;
+    r.defer_unpin_bytes = static_cast<size_t>(std::max(0L, env("LSEC_DEFER_UNPIN_MB", 256))) << 20;
     r.lone_blocks = static_cast<int>(std::min(16L, std::max(1L, env("LSEC_LONE_BLOCKS", 1))));
     r.server = env("LSEC_SERVER", 1) != 0;
     r.srv_nt_min = env("LSEC_SRV_NT_MIN_KB", -1) < 0 ? SIZE_MAX : static_cast<size_t>(env("LSEC_SRV_NT_MIN_KB", 0)) << 10;

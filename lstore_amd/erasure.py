@@ -80,7 +80,7 @@ EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan",
            "lsec_segment_straddle_bytes", "lsec_segment_read", "lsec_segment_inspect",
            "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count", "lsec_last_error", "lsec_plan_kernel",
            "lsec_set_kernel_variant", "lsec_set_host_devices", "lsec_hbm_copy_dev", "lsec_hbm_mix_dev", "lsec_prepare_encode", "lsec_plan_jit", "lsec_device_numa",
-           "lsec_set_tile_sharing", "lsec_tile_sharing")
+           "lsec_set_tile_sharing", "lsec_tile_sharing", "lsec_host_unpin_drain")
 
 # read / inspect flags and stripe states (include/lstore_ec.h)
 READ_PARANOID, MAGIC_LEGACY, INSPECT_FIX, MAX_DEVS = 1, 2, 4, 256
@@ -157,6 +157,8 @@ def lib():
     L.lsec_set_tile_sharing.argtypes = [C.c_int]
     L.lsec_set_tile_sharing.restype = None
     L.lsec_tile_sharing.restype = C.c_int
+    L.lsec_host_unpin_drain.argtypes = []
+    L.lsec_host_unpin_drain.restype = C.c_int
     L.lsec_set_host_devices.argtypes = [C.POINTER(C.c_int), C.c_int]
     L.lsec_hbm_copy_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_ulonglong, C.c_void_p]
     L.lsec_hbm_mix_dev.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_void_p]
@@ -566,3 +568,8 @@ def tile_sharing() -> int:
 
 def set_kernel_variant(bytewise: int = 0, bitsliced: int = 0) -> None:
     lib().lsec_set_kernel_variant(bytewise, bitsliced)
+
+
+def host_unpin_drain() -> None:
+    """lsec_host_unpin_drain: wait until registrations left to the background unpinner are dropped"""
+    lib().lsec_host_unpin_drain()
