@@ -287,12 +287,16 @@ class InPlacePin {
   bool pin(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
            long long C, size_t min_bytes, size_t min_run);
   void release();
+  bool held() const { return !held_.empty(); }
 
  private:
   static constexpr size_t kMaxRegions = 1024;
   std::vector<char *> held_;
   std::vector<std::pair<uintptr_t, uintptr_t>> claimed_;
 };
+
+// calls holding in-place registrations at this moment (this one included when it holds some)
+int in_place_calls();
 
 // DMA runs: pieces whose source and destination both continue the previous piece merge
 // into one copy (LStore's k data chunks of a stripe sit back to back in one cache page, so

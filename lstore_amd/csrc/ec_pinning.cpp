@@ -399,7 +399,9 @@ class Unpinner {
 };
 }  // namespace
 
-Unpinner *g_unpinner = nullptr;  // set once the first deferred release made it
+Unpinner *g_unpinner = nullptr;
+
+int in_place_calls() { return g_pins_held.load(std::memory_order_acquire); }  // set once the first deferred release made it
 
 void InPlacePin::release() {
   if (held_.empty() && claimed_.empty()) return;

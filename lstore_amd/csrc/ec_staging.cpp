@@ -236,18 +236,19 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
     if (b < C) cb = b;
   }
   const size_t slot_bytes = per_col * static_cast<size_t>(cb) * nb_max;
-  // One batch (a lone stripe's call, LStore's per-stripe pattern) has nothing to overlap: its H2D,
-  // kernel and D2H go in order on one stream, so two such calls at once hold two of the process's
-  // hardware queues instead of four (GPU_MAX_HW_QUEUES is 4 on this image, and the stripe server
-  // keeps one).  Measured level with two streams on LStore's 1 MiB per-stripe decodes (1 thread
-  // 32.6 vs 30.5 GiB/s, 2 threads 35.0 vs 36.3, inside the reference's own run-to-run spread;
-  // profiles/r05_v8_fnptr_one_stream.jsonl), so it stays an option: LSEC_ONE_STREAM=1.
-  static const bool one_stream_ok = [] {
+  // One batch (a lone stripe's call, LStore's per-stripe pattern) has nothing to overlap.  Pinned
+  // in place and alone, its H2D, kernel and D2H go in order on one stream: no cross-stream event
+  // between the H2D and the kernel (~20 us in the two-thread timeline, r05_v15); 1 MiB decodes at
+  // one thread 30.6 -> 32.4 / 33.1 GiB/s.  With other calls in flight, two streams let the copies
+  // of different calls interleave on the link: 43.6 / 44.6 against 40.5 / 40.5 at two threads
+  // (profiles/r05_v17_fnptr_one_stream_auto.jsonl).  LSEC_ONE_STREAM=1 / 0 forces either.
+  static const int one_stream_env = [] {
     const char *e = getenv("LSEC_ONE_STREAM");
-    return e && *e == '1';
+    return e && *e ? (*e == '1' ? 1 : 0) : -1;
   }();
   const bool one_batch = nb_max >= nstripes && cb >= C;
-  const hipStream_t s_h2d = one_stream_ok && one_batch ? stg->s_out : stg->s_in;
+  const bool one_stream = one_batch && (one_stream_env == 1 || (one_stream_env < 0 && inplace.held() && in_place_calls() == 1));
+  const hipStream_t s_h2d = one_stream ? stg->s_out : stg->s_in;
   const auto t_loop0 = now();
   std::vector<DmaRun> runs;
 
