@@ -361,6 +361,13 @@ class Unpinner {
     std::unique_lock<std::mutex> lk(mu_);
     done_.wait(lk, [&] { return pending_ == 0 && q_.empty(); });
   }
+  // at exit, before the runtime's own teardown (registered after it, so run before it): a bounded
+  // wait, since an unregister waits for work other threads may still have on the device
+  static void drain_at_exit() {
+    Unpinner &u = get();
+    std::unique_lock<std::mutex> lk(u.mu_);
+    u.done_.wait_for(lk, std::chrono::seconds(2), [&] { return u.pending_ == 0 && u.q_.empty(); });
+  }
   void put(std::vector<char *> held, std::vector<std::pair<uintptr_t, uintptr_t>> claimed, size_t bytes, size_t cap) {
     std::unique_lock<std::mutex> lk(mu_);
     done_.wait(lk, [&] { return pending_ == 0 || pending_ + bytes <= cap; });
@@ -375,7 +382,10 @@ class Unpinner {
     std::vector<std::pair<uintptr_t, uintptr_t>> claimed;
     size_t bytes;
   };
-  Unpinner() { std::thread([this] { loop(); }).detach(); }
+  Unpinner() {
+    std::thread([this] { loop(); }).detach();
+    std::atexit(drain_at_exit);
+  }
   void loop() {
     for (;;) {
       Item it;
