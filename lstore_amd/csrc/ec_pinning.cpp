@@ -508,6 +508,12 @@ void split_pieces(std::vector<lsec::CopyPiece> &v, uint64_t src, uint64_t dst, s
 // gaps hold one copy per 4 MiB run to 49.5 GB/s of the link's 57.6 H2D, and 1-2 MiB D2H runs to
 // 10-45 GB/s, where the strided copy runs at 57.6 / 57.0 (profiles/r05_v10_rect_probe.jsonl).
 // LSEC_DMA_2D=0 issues one copy per run.
+// Rows this wide already move at 0.97+ of the link one copy at a time, and strided copies of them
+// lost to plain copies when two processes shared the device's DMA engines (c4, Cauchy-good(10+4)
+// 4 MiB, 40 MiB rows, two ranks on one GPU: 14.9 against 23.2 GiB/s per rank pageable encode;
+// one process alone 51.3 against 48.7; profiles/r05_v18_c4_dma2d_ab.jsonl).
+constexpr size_t kMaxLatticeRow = 16u << 20;
+
 struct Lattice {
   size_t period = 0, rows = 0;
   ptrdiff_t sp = 0, dp = 0;
@@ -520,8 +526,9 @@ Lattice lattice_at(const std::vector<DmaRun> &v, size_t i) {
   for (size_t p = 1; p <= 8 && i + p < n; ++p) {
     const ptrdiff_t sp = v[i + p].src - v[i].src, dp = v[i + p].dst - v[i].dst;
     if (sp <= 0 || dp <= 0) continue;
-    bool fits = true;  // every lane's row fits its pitch
-    for (size_t l = 0; l < p && fits; ++l) fits = static_cast<size_t>(sp) >= v[i + l].bytes && static_cast<size_t>(dp) >= v[i + l].bytes;
+    bool fits = true;  // every lane's row fits its pitch, and is narrower than kMaxLatticeRow
+    for (size_t l = 0; l < p && fits; ++l)
+      fits = static_cast<size_t>(sp) >= v[i + l].bytes && static_cast<size_t>(dp) >= v[i + l].bytes && v[i + l].bytes < kMaxLatticeRow;
     if (!fits) continue;
     size_t rows = 1;
     for (;; ++rows) {

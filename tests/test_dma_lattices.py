@@ -125,3 +125,15 @@ def test_irregular_and_mixed_runs(built):
 
 def test_empty(built):
     assert plan([]) == []
+
+
+def test_wide_rows_go_one_by_one(built):
+    # rows of 16 MiB and more: one copy each (kMaxLatticeRow)
+    runs = stripes(8, 10, 4, 4 * MiB, range(10))  # 40 MiB rows
+    g = plan(runs)
+    check_cover(runs, g)
+    assert all(x[2] == 1 for x in g)
+    runs = stripes(8, 4, 2, 4 * MiB - 4096, range(4))  # just under 16 MiB
+    g = plan(runs)
+    check_cover(runs, g)
+    assert g[0][:3] == (0, 1, 8)
