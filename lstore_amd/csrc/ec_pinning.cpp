@@ -409,9 +409,9 @@ class Unpinner {
 };
 }  // namespace
 
-Unpinner *g_unpinner = nullptr;
+std::atomic<Unpinner *> g_unpinner{nullptr};  // set once the first deferred release made it
 
-int in_place_calls() { return g_pins_held.load(std::memory_order_acquire); }  // set once the first deferred release made it
+int in_place_calls() { return g_pins_held.load(std::memory_order_acquire); }
 
 void InPlacePin::release() {
   if (held_.empty() && claimed_.empty()) return;
@@ -420,7 +420,7 @@ void InPlacePin::release() {
   // deferred only while another call is in flight: alone, the unregister is immediate (the runtime
   // re-registers recently registered pages in microseconds, and nothing else of ours is running)
   if (cap > 0 && others && !held_.empty()) {
-    g_unpinner = &Unpinner::get();
+    g_unpinner.store(&Unpinner::get(), std::memory_order_release);
     size_t bytes = 0;
     for (const auto &c : claimed_) bytes += c.second - c.first;
     Unpinner::get().put(std::move(held_), std::move(claimed_), bytes, cap);
@@ -611,7 +611,7 @@ hipError_t issue_runs(const std::vector<DmaRun> &v, hipMemcpyKind kind, hipStrea
 // include/lstore_ec.h: wait until every in-place registration a call left to the background
 // unpinner is dropped (before the caller registers host memory with HIP itself)
 extern "C" int lsec_host_unpin_drain(void) {
-  if (lsec::eng::g_unpinner) lsec::eng::g_unpinner->drain();
+  if (lsec::eng::Unpinner *u = lsec::eng::g_unpinner.load(std::memory_order_acquire)) u->drain();
   return 0;
 }
 
