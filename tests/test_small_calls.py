@@ -281,3 +281,69 @@ def test_stale_caller_hip_error_is_not_taken_for_a_launch_failure(cuda):
                          timeout=110)
     assert out.returncode == 0 and out.stdout.strip().endswith("ok"), (out.stdout[-500:], out.stderr[-800:])
     assert "retried with direct copies" not in out.stderr, out.stderr[-800:]
+
+
+UNPIN_SCRIPT = r"""
+import ctypes, sys, threading
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import lstore_amd as L
+from lstore_amd import erasure as E
+import oracle as O
+hip = ctypes.CDLL("libamdhip64.so")
+k, m, C = 6, 3, 1 << 20
+plan = L.Plan.for_chunk(L.CAUCHY_GOOD, k, m, C)
+plan.prepare_encode()
+plan.prepare_decode([0])
+errors, arenas = [], []
+lock = threading.Lock()
+
+
+def worker(t):
+    rng = np.random.default_rng(t)
+    try:
+        for it in range(30):
+            # a fresh page-aligned pageable stripe per call, pinned in place by the call
+            a = np.zeros(9 * C + 4096, np.uint8)
+            off = (-a.ctypes.data) % 4096
+            d = a[off:off + 9 * C].reshape(9, C)
+            d[:k] = rng.integers(0, 256, (k, C), dtype=np.uint8)
+            plan.encode_block([d[j] for j in range(9)])
+            if not np.array_equal(d[k:], O.encode(L.CAUCHY_GOOD, d[:k], m, plan.packet_size)):
+                errors.append((t, it, "encode"))
+            want = d[0].copy()
+            d[0] = 0
+            plan.decode_block([d[j] for j in range(9)], [0])
+            if not np.array_equal(d[0], want):
+                errors.append((t, it, "decode"))
+            with lock:
+                arenas.append(d)
+    except Exception as e:
+        errors.append((t, repr(e)))
+
+
+th = [threading.Thread(target=worker, args=(t,)) for t in range(3)]
+for x in th:
+    x.start()
+for x in th:
+    x.join()
+assert not errors, errors[:5]
+# every registration a call left to the background unpinner is gone after the drain: the caller
+# can now register (and release) any of those ranges itself
+E.host_unpin_drain()
+for d in arenas[-24:]:
+    p, n = ctypes.c_void_p(d.ctypes.data), ctypes.c_size_t(d.nbytes)
+    assert hip.hipHostRegister(p, n, 0) == 0
+    assert hip.hipHostUnregister(p) == 0
+print("ok", len(arenas))
+"""
+
+
+def test_background_unpinner_and_drain(cuda):
+    """Three threads of per-stripe 1 MiB calls on fresh pageable stripes (pinned in place; with
+    other calls in flight, each call's registration is dropped by the background unpinner after it
+    returns, ec_pinning.cpp): every result equals the oracle's, and after lsec_host_unpin_drain()
+    the caller can register and release those ranges itself (INTEGRATION.md "Host buffers")."""
+    out = subprocess.run([sys.executable, "-c", UNPIN_SCRIPT, ROOT], capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, (out.stdout[-500:], out.stderr[-1500:])
+    assert out.stdout.strip().startswith("ok"), out.stdout[-300:]
