@@ -297,6 +297,53 @@ def host_path_rate(plan, k, m, C, lost, nstripes, pinned=False, reps=3, barrier=
                      "pageable host buffers -> pinned staging -> H2D -> kernel -> D2H -> host")}
 
 
+# the generic kernel of each lsec_plan_kernel kind (include/lstore_ec.h)
+KERNEL_KINDS = {1: "k_gf8_bytewise", 2: "k_gf8_bitsliced", 3: "k_bitmatrix", 4: "k_gfw_transposed", 5: "k_gfw_bitsliced"}
+
+
+def kernel_label(kind, jit, measured=None):
+    """roofline.kernel: the encode kernel that actually ran.  `measured` is the kernel the in-run
+    PMC pass saw write the most (the encode), named as rocprofv3 reports it; otherwise the plan
+    says: its compiled network (lsec_xornet: XOR networks for wide RS codes and w = 16 / 32,
+    packet networks for Cauchy and the liberation family, lsec_plan_jit) or the generic kernel of
+    its kind."""
+    if measured:
+        return f"{measured} (encode; named by the in-run PMC pass)"
+    generic = KERNEL_KINDS.get(kind, f"kind {kind}")
+    if jit:
+        return f"lsec_xornet (encode: compiled network in place of {generic})"
+    return f"{generic} (encode)"
+
+
+# SURVEY.md §8d's synthetic input: the splitmix64 stream from seed 0x4C53544F5245, stripe s's k
+# data chunks at counter base s*k*C/8 (tests/patterns.py is the numpy statement of it)
+SPLITMIX_SEED = 0x4C53544F5245
+
+
+def _i64(x):
+    x &= (1 << 64) - 1
+    return x - (1 << 64) if x >= 1 << 63 else x
+
+
+def splitmix_rows(torch, rows, counter0, seed=SPLITMIX_SEED, words_per_pass=1 << 25):
+    """rows (uint8 [R, C], C % 8 == 0, rows may be strided) <- the splitmix64 byte stream from
+    word counter0 on, row after row: word i (1-based from counter0 + 1) is
+    mix(seed + i * 0x9E3779B97F4A7C15).  int64 arithmetic wraps as uint64 does; the right shifts
+    are masked to be logical."""
+    R, C = rows.shape
+    w = C // 8
+    step = max(1, words_per_pass // w)
+    for r0 in range(0, R, step):
+        r1 = min(R, r0 + step)
+        z = torch.arange(counter0 + r0 * w + 1, counter0 + r1 * w + 1, dtype=torch.int64, device=rows.device)
+        z = z * _i64(0x9E3779B97F4A7C15) + _i64(seed)
+        z = (z ^ ((z >> 30) & ((1 << 34) - 1))) * _i64(0xBF58476D1CE4E5B9)
+        z = (z ^ ((z >> 27) & ((1 << 37) - 1))) * _i64(0x94D049BB133111EB)
+        z = z ^ ((z >> 31) & ((1 << 33) - 1))
+        rows[r0:r1].copy_(z.view(torch.uint8).view(r1 - r0, C))
+        del z
+
+
 # ----------------------------------------------------------------------------- the engine
 class HipEngine:
     """The device-resident hot path: liblstore_ec.so's lsec_encode_dev / lsec_decode_dev on
@@ -380,10 +427,13 @@ class HipEngine:
         torch, a = self.torch, self.a
         k, m, C = a.k, a.m, a.chunk
         row = C + max(pad, self.room)
-        g = torch.Generator(device=self.dev).manual_seed(seed)
-        self.flat = (torch.randint(0, 256, (N * k * row,), dtype=torch.uint8, device=self.dev, generator=g),
+        self.flat = (torch.empty((N * k * row,), dtype=torch.uint8, device=self.dev),
                      torch.empty((N * m * row,), dtype=torch.uint8, device=self.dev),
                      torch.empty((N * row,), dtype=torch.uint8, device=self.dev))
+        # the data chunks (global stripes first .. first+N-1) as the headline layout places them
+        # (views(N, pad)), from SURVEY §8d's splitmix64 stream; the bytes between them stay as
+        # allocated (only the layout A/B's timing passes read them)
+        splitmix_rows(torch, self.flat[0][: N * k * (C + pad)].view(N * k, C + pad)[:, :C], first * k * C // 8)
         return self.views(N, pad)
 
     def views(self, N, pad):
@@ -560,6 +610,8 @@ class HipEngine:
             xplan.close()
             del xd, xp
             self.drop()
+            out["hbm_copy_ref"]["decode_shape"] = self.decode_shape(N, timed)
+            self.drop()
         if rank == 0 and world == 1:
             # the reference CPU path is timed at N=1 only (at N>1 it would only delay the ranks' exit)
             out["cpu_baseline"] = None if a.no_cpu else cpu_baseline(self.method, k, m, C, self.P, a.lost, a.cpu_seconds)
@@ -571,8 +623,62 @@ class HipEngine:
             out["host_path"] = host
         return out
 
+    def decode_shape(self, N, timed):
+        """The decode's own memory shape in a kernel that shares no code with it
+        (lsec_hbm_decode_shape_dev: XOR of the decode's k survivors into one output, every IT / grab
+        / XCD-order variant), timed on one fresh allocation together with the real decode over the
+        same buffers, so both draw the same placement mode."""
+        torch, a, lib, E = self.torch, self.a, self.lib, self.E
+        k, m, C = a.k, a.m, a.chunk
+        dec_hbm = (k + 1) * C * N
+        dd = self.random_bytes((N, k, C))
+        dq = torch.empty((N, m, C), dtype=torch.uint8, device=self.dev)
+        dr = torch.empty((N, 1, C), dtype=torch.uint8, device=self.dev)
+        refs = [(dd.data_ptr() + j * C, k * C) for j in range(k)] + [(dq.data_ptr() + r * C, m * C) for r in range(m)]
+        enc_arr = self.plan.shard_refs(refs)
+        dec_refs = list(refs)
+        dec_refs[a.lost] = (dr.data_ptr(), C)
+        dec_arr = self.plan.shard_refs(dec_refs)
+        if lib.lsec_encode_dev(self.plan.ptr, enc_arr, N, C, self.sh):  # consistent parity
+            raise E.ErasureError(E.last_error())
+        survivors = [refs[j] for j in range(k + m) if j != a.lost][:k]
+        probe_arr = self.plan.shard_refs(survivors + [(dr.data_ptr(), C)])
+
+        def decode():
+            if lib.lsec_decode_dev(self.plan.ptr, dec_arr, N, C, self.er, self.sh):
+                raise E.ErasureError(E.last_error())
+
+        variants = {}
+        t_dec = timed(decode)
+        for remap in (0, 1):
+            for it in (1, 2, 4):
+                if C % (4096 * it):
+                    continue
+                for g in (1, 2, 4):
+                    v = it | g << 4 | remap << 8
+
+                    def probe(v=v):
+                        if lib.lsec_hbm_decode_shape_dev(probe_arr, k, N, C, v, self.sh):
+                            raise E.ErasureError(E.last_error())
+
+                    variants[f"it{it}_g{g}_{'xcd' if remap else 'rr'}"] = timed(probe)
+        t_dec2 = timed(decode)  # the decode again after the sweep: the allocation's rate held
+        del dd, dq, dr
+        if not variants:
+            return None
+        best = min(variants, key=variants.get)
+        td = min(t_dec, t_dec2)
+        return {"what": "XOR of the decode's k survivors into one shard over N stripes in a kernel sharing no code with "
+                        "the coding kernels (lsec_hbm_decode_shape_dev), every variant; the real decode timed before "
+                        "and after on the same buffers",
+                "best_variant": best, "best_frac": round(dec_hbm / variants[best] / HBM_PEAK, 4),
+                "decode_frac_same_buffers": round(dec_hbm / td / HBM_PEAK, 4),
+                "decode_frac_before_after": [round(dec_hbm / t_dec / HBM_PEAK, 4), round(dec_hbm / t_dec2 / HBM_PEAK, 4)],
+                "decode_vs_shape": round(variants[best] / td, 3),
+                "variants_frac": {key: round(dec_hbm / t / HBM_PEAK, 4) for key, t in variants.items()}}
+
     def kernel_name(self):
-        return "gf8_bytewise (encode)" if self.kernel == 1 else "gf8_bitsliced (encode)"
+        return kernel_label(self.kernel, self.plan.jit(), (getattr(self.a, "traffic_live", None) or {}).get("kernel"))
 
     def traffic(self, N):
         live = getattr(self.a, "traffic_live", None)
@@ -710,7 +816,7 @@ def run_rank(a, rank, world, local, engine_cls=HipEngine):
             "scaling": "strong" if a.total_stripes > 0 else "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (torch.randint bytes, resident in HBM)",
+            "data": "synthetic: SURVEY §8d splitmix64 stream, seed 0x4C53544F5245, stripe s at word s*k*C/8, resident in HBM",
             "config": {"workload": f"{method}({k}+{m}) encode + decode(lost shard {a.lost}), C={C} B per shard, "
                                    f"{N} stripes/GPU, k*C={k * C} B user data per stripe",
                        "method": method, "k": k, "m": m, "chunk_bytes": C, "packet_size": eng.P,

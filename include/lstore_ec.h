@@ -262,12 +262,12 @@ void lsec_set_kernel_variant(int bytewise_variant, int bitsliced_variant);  /* t
  * mode. */
 void lsec_set_tile_sharing(int mode);
 int lsec_tile_sharing(void);
-/* Pageable host chunks a call pins in place (hipHostRegister) are unregistered when the call ends;
- * while other calls hold registrations of their own, a background thread does it instead, shortly
- * after the call returns (hipHostUnregister waits until the whole device is idle, so calls on
- * several threads would otherwise wait for each other's transfers; LSEC_DEFER_UNPIN_MB caps what
- * may be pending, 0 turns it off).  A caller that registers host memory with HIP itself, or hands
- * such memory to another HIP user, calls this first: it returns when nothing is pending.  0. */
+/* Pageable host chunks a call pins in place (hipHostRegister) are unregistered before the call
+ * returns.  Opt-in (LSEC_DEFER_UNPIN_MB > 0, for a process where this library is the only HIP
+ * user): while other calls hold registrations of their own, a background thread does it instead,
+ * shortly after the call returns (hipHostUnregister waits until the whole device is idle).  With
+ * that on, a caller that registers host memory with HIP itself, or hands memory it may have freed
+ * and reallocated to another HIP user, calls this first: it returns when nothing is pending.  0. */
 int lsec_host_unpin_drain(void);
 /* Measurement probe, not part of the coding path: enqueue a streaming device copy dst <- src
  * (bytes a multiple of 16, 16-byte aligned device pointers) on `stream` with the coding kernels'
@@ -278,6 +278,13 @@ int lsec_hbm_copy_dev(void *dst, const void *src, unsigned long long bytes, void
  * arithmetic, which bench.py times beside the encode.  0 / -1. */
 int lsec_hbm_mix_dev(const lsec_shard_t *shards, int k, int m, int nstripes, long long block_size, void *stream);
 
+/* Measurement probe: for every stripe, shards[k] <- XOR of shards[0..k), in a kernel that shares
+ * no code with the coding kernels: the single-erasure decode's k-read : 1-write HBM traffic with
+ * the plainest streaming code.  variant = IT | G << 4 | REMAP << 8: IT (1, 2, 4) 16-byte steps
+ * per lane, G (1, 2, 4) tiles of 4096 * IT bytes per workgroup, REMAP 1 = XCD-contiguous grabs;
+ * block_size a multiple of 4096 * IT.  bench.py times every variant beside the decode.  0 / -1. */
+int lsec_hbm_decode_shape_dev(const lsec_shard_t *shards, int k, int nstripes, long long block_size, int variant,
+                              void *stream);
 #ifdef __cplusplus
 }
 #endif

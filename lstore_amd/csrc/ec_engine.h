@@ -151,10 +151,13 @@ struct RouteTable {
                                // takes route 4 pinned in place (DMA, no packing) ...
   size_t own_dma_min_bytes;    // 1 MiB: ... when the call has this many bytes ...
   size_t own_dma_min_run;      // LSEC_OWN_DMA_MIN_RUN_KB = 1024: ... and its DMA runs average this
-  size_t defer_unpin_bytes;    // LSEC_DEFER_UNPIN_MB = 256: while another call holds in-place
-                               // registrations, a call's own are dropped by a background thread after
-                               // it returns, at most this many bytes pending (hipHostUnregister waits
-                               // for the whole device to idle); 0 = always at the end of the call
+  size_t defer_unpin_bytes;    // LSEC_DEFER_UNPIN_MB = 0 (off): > 0 lets a background thread drop a
+                               // call's in-place registrations after it returns while another call
+                               // holds registrations, at most this many bytes pending
+                               // (hipHostUnregister waits for the whole device to idle).  Off by
+                               // default: a registration that outlives its call maps pages the caller
+                               // may free and reuse, and another HIP user in the process would take
+                               // them for page-locked memory
   int lone_blocks;             // LSEC_LONE_BLOCKS = 1: a lone stripe DMA'd in place moves in this many
                                // column blocks (block b+1's H2D under block b's kernel and D2H)
   bool server;                 // LSEC_SERVER = 1: route 1 on

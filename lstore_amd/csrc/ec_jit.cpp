@@ -992,12 +992,18 @@ void compile_source(const std::string &src, std::string &err, std::vector<char> 
     reply.insert(reply.end(), buf, buf + r);
   }
   close(out[0]);
-  int status = 0;
-  while (waitpid(pid, &status, 0) < 0 && errno == EINTR) {
+  // Wait for the exit without reaping (WNOWAIT), take the pid out of g_children, and only then
+  // reap: until the reap the pid stays a zombie of ours, so stop_compiles can never SIGKILL a pid
+  // the system has already handed to another process
+  siginfo_t si;
+  while (waitid(P_PID, static_cast<id_t>(pid), &si, WEXITED | WNOWAIT) < 0 && errno == EINTR) {
   }
   {
     std::lock_guard<std::mutex> lk(g_child_mu);
     g_children.erase(pid);
+  }
+  int status = 0;
+  while (waitpid(pid, &status, 0) < 0 && errno == EINTR) {
   }
   uint64_t n = 0;
   if (reply.size() >= 13)

@@ -199,6 +199,11 @@ hipError_t launch_hbm_copy(void *dst, const void *src, uint64_t bytes, hipStream
 // HBM probe (measurement only): out[r] = XOR of the K inputs for every stripe (a.K, a.R <= kMaxR,
 // a.in / a.out / a.nstripes / a.size): the encode's K-read : R-write traffic without its arithmetic.
 hipError_t launch_hbm_mix(const ApplyArgs &a, hipStream_t stream);
+// HBM probe (measurement only): out = XOR of the K inputs for every stripe, in a kernel that shares
+// no code with the coding kernels (the decode's K-read : 1-write shape); variant = IT | G << 4 |
+// REMAP << 8: IT 16-byte steps per lane, G tiles per block, XCD-contiguous grabs (ec_kernels.hip).
+hipError_t launch_probe_xor(const ShardRef *in, int K, ShardRef out, int nstripes, int64_t size, int variant,
+                            hipStream_t stream);
 
 // Host helper: fill one cell for coefficient c.
 void make_cell(uint8_t c, CoefCell &cell);

@@ -121,21 +121,31 @@ unsigned *tile_queue_slot(hipStream_t st, uint64_t ntiles) {
   std::call_once(g_queue_once[dev], [dev] {
     const size_t bytes = sizeof(unsigned) * kTileQueueWords * kTileQueueRing;
     void *p = nullptr;
-    int cus = 0, cur = -1;
-    // on st's device, which need not be the calling thread's current one
-    if (quiet([&] { return hipGetDevice(&cur); }) != hipSuccess) return;
-    if (cur != dev && quiet([&] { return hipSetDevice(dev); }) != hipSuccess) return;
-    struct Restore {
-      int cur, dev;
-      ~Restore() {
-        if (cur != dev) (void)quiet([&] { return hipSetDevice(cur); });
+    int cus = 0;
+    // On st's device, which need not be the calling thread's current one.  One quiet() call does
+    // the switch, the allocation, the clear and the switch back, so all of it runs on one thread:
+    // with a caller's error pending quiet() runs its call on the helper thread, and a device
+    // switched there would not be the one a later quiet() call allocates on.
+    const hipError_t e = quiet([&] {
+      int cur = -1;
+      hipError_t r = hipGetDevice(&cur);
+      if (r != hipSuccess) return r;
+      if (cur != dev && (r = hipSetDevice(dev)) != hipSuccess) return r;
+      r = hipMalloc(&p, bytes);
+      if (r == hipSuccess) r = hipMemset(p, 0, bytes);
+      if (r == hipSuccess) r = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (r != hipSuccess && p) {
+        (void)hipFree(p);
+        p = nullptr;
       }
-    } restore{cur, dev};
-    if (quiet([&] { return hipMalloc(&p, bytes); }) != hipSuccess) return;
-    if (quiet([&] { return hipMemset(p, 0, bytes); }) != hipSuccess ||
-        quiet([&] { return hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev); }) != hipSuccess ||
-        cus <= 0) {
-      (void)hipFree(p);
+      if (cur != dev) {
+        const hipError_t back = hipSetDevice(cur);
+        if (r == hipSuccess) r = back;
+      }
+      return r;
+    });
+    if (e != hipSuccess || cus <= 0 || !p) {
+      if (p) (void)quiet([&] { return hipFree(p); });
       return;
     }
     g_cus[dev] = cus;
@@ -465,6 +475,67 @@ __global__ __launch_bounds__(kBlock) void k_hbm_mix(ApplyArgs a) {
   });
 }
 
+// Decode-shape probe (measurement only; shares no code with the coding kernels or their tile
+// helpers): per stripe, out = XOR of the K inputs -- the single-erasure decode's K reads : 1 write
+// per column with the plainest streaming code.  A lane moves 16 B per step, IT steps kBlock*16 B
+// apart (a tile is kBlock*16*IT bytes of every shard); block b takes G consecutive tiles (a grab)
+// of a static partition, the grabs dealt XCD-contiguous (REMAP: XCD x = blocks b % 8 == x gets an
+// eighth of the grabs in order) or round-robin; all K*IT loads of a tile are issued before the
+// XOR.  bench.py times every (IT, G, REMAP) beside the decode as the decode's own ceiling.
+struct ProbeXorArgs {
+  int K;
+  int nstripes;
+  int64_t size;  // a multiple of kBlock * 16 * IT
+  int grab;
+  int remap;
+  ShardRef in[kMaxK];
+  ShardRef out;
+};
+
+template <int KC, int IT>
+__global__ __launch_bounds__(kBlock) void k_probe_xor(ProbeXorArgs a) {
+  constexpr int64_t kStep = kBlock * 16, kTile = kStep * IT;
+  const int K = KC ? KC : a.K;
+  const uint32_t tps = static_cast<uint32_t>(a.size / kTile);
+  const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
+  const uint32_t G = static_cast<uint32_t>(a.grab), ngrabs = (ntiles + G - 1) / G;
+  uint32_t g = blockIdx.x;
+  if (a.remap) {
+    const uint32_t nb = gridDim.x, per = nb >> 3, rem = nb & 7, x = blockIdx.x & 7;
+    g = x * per + min(x, rem) + (blockIdx.x >> 3);
+  }
+  for (; g < ngrabs; g += gridDim.x) {
+    const uint32_t t1 = min(ntiles, (g + 1) * G);
+    for (uint32_t t = g * G; t < t1; ++t) {
+      const uint32_t s = t / tps;
+      const int64_t off = static_cast<int64_t>(t - s * tps) * kTile + threadIdx.x * 16;
+      u32x4 acc[IT];
+#pragma unroll
+      for (int it = 0; it < IT; ++it) acc[it] = 0u;
+      if constexpr (KC > 0) {
+        u32x4 v[KC][IT];
+#pragma unroll
+        for (int j = 0; j < KC; ++j)
+#pragma unroll
+          for (int it = 0; it < IT; ++it)
+            v[j][it] = __builtin_nontemporal_load(gptr<u32x4>(a.in[j].base + s * a.in[j].stride + off + it * kStep));
+#pragma unroll
+        for (int j = 0; j < KC; ++j)
+#pragma unroll
+          for (int it = 0; it < IT; ++it) acc[it] ^= v[j][it];
+      } else {
+        for (int j = 0; j < K; ++j)
+#pragma unroll
+          for (int it = 0; it < IT; ++it)
+            acc[it] ^= __builtin_nontemporal_load(gptr<u32x4>(a.in[j].base + s * a.in[j].stride + off + it * kStep));
+      }
+#pragma unroll
+      for (int it = 0; it < IT; ++it)
+        __builtin_nontemporal_store(acc[it], gptr_w<u32x4>(a.out.base + s * a.out.stride + off + it * kStep));
+    }
+  }
+}
+
 // A small grid striding over the pieces, every lane holding its 4 x 16 B of a piece in flight
 // before storing: enough bytes in flight for PCIe, while the H2D and D2H launches (on two
 // streams) and the coding kernel between them all keep room on the CUs.  (One block per piece
@@ -548,6 +619,32 @@ hipError_t launch_hbm_mix(const ApplyArgs &a, hipStream_t st) {
   const uint64_t ntiles = ((a.size + tile - 1) / tile) * static_cast<uint64_t>(a.nstripes);
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   return launch_tiled(&k_hbm_mix, default_grid(ntiles), st, a);
+}
+
+// variant = IT | G << 4 | REMAP << 8 (IT, G in {1, 2, 4})
+hipError_t launch_probe_xor(const ShardRef *in, int K, ShardRef out, int nstripes, int64_t size, int variant,
+                            hipStream_t st) {
+  const int IT = variant & 15, G = (variant >> 4) & 15, remap = (variant >> 8) & 1;
+  if (K < 1 || K > kMaxK || nstripes < 0 || (IT != 1 && IT != 2 && IT != 4) || (G != 1 && G != 2 && G != 4) ||
+      size % (static_cast<int64_t>(kBlock) * 16 * IT) != 0)
+    return hipErrorInvalidValue;
+  if (nstripes == 0 || size == 0) return hipSuccess;
+  ProbeXorArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.K = K;
+  a.nstripes = nstripes;
+  a.size = size;
+  a.grab = G;
+  a.remap = remap;
+  for (int j = 0; j < K; ++j) a.in[j] = in[j];
+  a.out = out;
+  const uint64_t ntiles = static_cast<uint64_t>(size / (static_cast<int64_t>(kBlock) * 16 * IT)) * nstripes;
+  const uint64_t grid = (ntiles + G - 1) / G;
+  if (grid >= (1ull << 31)) return hipErrorInvalidValue;
+  const auto go = [&](auto kern) { return launch_kernel(kern, dim3(static_cast<unsigned>(grid)), dim3(kBlock), st, a); };
+  if (K == 6) return IT == 1 ? go(&k_probe_xor<6, 1>) : IT == 2 ? go(&k_probe_xor<6, 2>) : go(&k_probe_xor<6, 4>);
+  if (K == 10) return IT == 1 ? go(&k_probe_xor<10, 1>) : IT == 2 ? go(&k_probe_xor<10, 2>) : go(&k_probe_xor<10, 4>);
+  return IT == 1 ? go(&k_probe_xor<0, 1>) : IT == 2 ? go(&k_probe_xor<0, 2>) : go(&k_probe_xor<0, 4>);
 }
 
 hipError_t launch_gather(const GatherPiece *list, int n, char *dst, hipStream_t st) {

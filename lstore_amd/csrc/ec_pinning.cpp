@@ -359,18 +359,26 @@ class Unpinner {
   // until nothing is pending (lsec_host_unpin_drain)
   void drain() {
     std::unique_lock<std::mutex> lk(mu_);
-    done_.wait(lk, [&] { return pending_ == 0 && q_.empty(); });
+    done_.wait(lk, [&] { return exiting_ || (pending_ == 0 && q_.empty()); });
   }
   // at exit, before the runtime's own teardown (registered after it, so run before it): a bounded
   // wait, since an unregister waits for work other threads may still have on the device
+  // After the wait, whatever is still queued is dropped with no runtime call: the thread starts no
+  // unregister once the runtime's teardown may be under way (the registrations go
+  // with the process).
   static void drain_at_exit() {
     Unpinner &u = get();
     std::unique_lock<std::mutex> lk(u.mu_);
     u.done_.wait_for(lk, std::chrono::seconds(2), [&] { return u.pending_ == 0 && u.q_.empty(); });
+    u.exiting_ = true;
+    u.q_.clear();
+    u.work_.notify_all();
+    u.done_.notify_all();
   }
   void put(std::vector<char *> held, std::vector<std::pair<uintptr_t, uintptr_t>> claimed, size_t bytes, size_t cap) {
     std::unique_lock<std::mutex> lk(mu_);
-    done_.wait(lk, [&] { return pending_ == 0 || pending_ + bytes <= cap; });
+    done_.wait(lk, [&] { return exiting_ || pending_ == 0 || pending_ + bytes <= cap; });
+    if (exiting_) return;  // (the process is exiting: the registrations go with it)
     q_.push_back({std::move(held), std::move(claimed), bytes});
     pending_ += bytes;
     work_.notify_one();
@@ -391,7 +399,8 @@ class Unpinner {
       Item it;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        work_.wait(lk, [&] { return !q_.empty(); });
+        work_.wait(lk, [&] { return !q_.empty() || exiting_; });
+        if (exiting_) return;
         it = std::move(q_.front());
         q_.pop_front();
       }
@@ -406,6 +415,7 @@ class Unpinner {
   std::condition_variable work_, done_;
   std::deque<Item> q_;
   size_t pending_ = 0;
+  bool exiting_ = false;  // set by drain_at_exit: no unregister starts after it
 };
 }  // namespace
 

@@ -42,7 +42,7 @@ const RouteTable &routes() {
     r.own_dma_max = static_cast<int>(std::max(0L, env("LSEC_OWN_DMA_MAX", 2)));
     r.own_dma_min_bytes = 1u << 20;
     r.own_dma_min_run = static_cast<size_t>(std::max(0L, env("LSEC_OWN_DMA_MIN_RUN_KB", 1024))) << 10;
-    r.defer_unpin_bytes = static_cast<size_t>(std::max(0L, env("LSEC_DEFER_UNPIN_MB", 256))) << 20;
+    r.defer_unpin_bytes = static_cast<size_t>(std::max(0L, env("LSEC_DEFER_UNPIN_MB", 0))) << 20;
     r.lone_blocks = static_cast<int>(std::min(16L, std::max(1L, env("LSEC_LONE_BLOCKS", 1))));
     r.server = env("LSEC_SERVER", 1) != 0;
     r.srv_nt_min = env("LSEC_SRV_NT_MIN_KB", -1) < 0 ? SIZE_MAX : static_cast<size_t>(env("LSEC_SRV_NT_MIN_KB", 0)) << 10;
@@ -656,6 +656,18 @@ int lsec_hbm_mix_dev(const lsec_shard_t *shards, int k, int m, int nstripes, lon
   return 0;
 }
 
+
+int lsec_hbm_decode_shape_dev(const lsec_shard_t *shards, int k, int nstripes, long long block_size, int variant,
+                              void *stream) {
+  if (!shards || k < 1 || k > lsec::kMaxK || nstripes < 0 || block_size < 0)
+    return fail("lsec_hbm_decode_shape_dev: bad arguments (k=%d nstripes=%d block_size=%lld)", k, nstripes, block_size);
+  lsec::ShardRef in[lsec::kMaxK];
+  for (int j = 0; j < k; ++j) in[j] = {reinterpret_cast<uint64_t>(shards[j].base), shards[j].stride};
+  const lsec::ShardRef out = {reinterpret_cast<uint64_t>(shards[k].base), shards[k].stride};
+  const hipError_t e = lsec::launch_probe_xor(in, k, out, nstripes, block_size, variant, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return fail("lsec_hbm_decode_shape_dev: %s", hipGetErrorString(e));
+  return 0;
+}
 
 int lsec_device_numa(int dev, int *node, int *cpus, int max_cpus) {
   int n = 0;

@@ -88,7 +88,36 @@ Staging *acquire_staging(int dev) {
   return s;
 }
 
+// Device halves larger than the packed geometry's (the in-place DMA geometry, dev_staging_bytes:
+// up to ~256 MiB a slot) are kept by at most kKeepLarge pooled stagings per device; a staging that
+// comes back with them beyond that gives them up (the next large call regrows them).  Otherwise the
+// HBM the pool holds for the life of the process grew with the peak count of concurrent large
+// pinned calls: 16 threads of RS(6+3) 1 MiB batches kept ~12 GiB.
+constexpr int kKeepLarge = 2;
+
+bool large_device_half(const Staging *s) {
+  for (const auto &sl : s->slot)
+    if (sl.cap > routes().staging_bytes / 2) return true;
+  return false;
+}
+
 void release_staging(Staging *s) {
+  bool shrink = false;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (large_device_half(s)) {
+      int large = 0;
+      for (const Staging *o : g_pool[s->dev]) large += large_device_half(o);
+      shrink = large >= kKeepLarge;
+    }
+  }
+  if (shrink)
+    for (auto &sl : s->slot)
+      if (sl.cap > routes().staging_bytes / 2) {
+        (void)quiet([&] { return hipFree(sl.d); });  // (every slot was drained before the release)
+        sl.d = nullptr;
+        sl.cap = 0;
+      }
   std::lock_guard<std::mutex> lk(g_pool_mu);
   g_pool[s->dev].push_back(s);
 }
@@ -410,3 +439,21 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
 
 }  // namespace eng
 }  // namespace lsec
+
+// Test hook, not part of include/*.h: the staging pool of device dev -- out[0] = pooled stagings,
+// out[1] = those holding device halves larger than the packed geometry's, out[2] = device bytes
+// their slots hold.  0.
+extern "C" int lsec_test_staging_pool(int dev, long long *out) {
+  using namespace lsec::eng;
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  long long n = 0, large = 0, bytes = 0;
+  for (const Staging *s : g_pool[dev]) {
+    ++n;
+    large += large_device_half(s);
+    for (const auto &sl : s->slot) bytes += static_cast<long long>(sl.cap);
+  }
+  out[0] = n;
+  out[1] = large;
+  out[2] = bytes;
+  return 0;
+}

@@ -80,7 +80,7 @@ EXPORTS = ("nearest_prime", "et_method_type", "et_new_plan", "et_generate_plan",
            "lsec_segment_straddle_bytes", "lsec_segment_read", "lsec_segment_inspect",
            "lsec_prepare_decode", "lsec_abi_version", "lsec_device_count", "lsec_last_error", "lsec_plan_kernel",
            "lsec_set_kernel_variant", "lsec_set_host_devices", "lsec_hbm_copy_dev", "lsec_hbm_mix_dev", "lsec_prepare_encode", "lsec_plan_jit", "lsec_device_numa",
-           "lsec_set_tile_sharing", "lsec_tile_sharing", "lsec_host_unpin_drain")
+           "lsec_set_tile_sharing", "lsec_tile_sharing", "lsec_host_unpin_drain", "lsec_hbm_decode_shape_dev")
 
 # read / inspect flags and stripe states (include/lstore_ec.h)
 READ_PARANOID, MAGIC_LEGACY, INSPECT_FIX, MAX_DEVS = 1, 2, 4, 256
@@ -162,6 +162,7 @@ def lib():
     L.lsec_set_host_devices.argtypes = [C.POINTER(C.c_int), C.c_int]
     L.lsec_hbm_copy_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_ulonglong, C.c_void_p]
     L.lsec_hbm_mix_dev.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_void_p]
+    L.lsec_hbm_decode_shape_dev.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_longlong, C.c_int, C.c_void_p]
     L.lsec_device_numa.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int]
     L.lsec_test_numa_for_bus.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int]
     L.lsec_test_server_hold.restype = C.c_longlong

@@ -1274,3 +1274,60 @@ def test_tile_sharing_concurrent_streams(cuda):
         for t in ts:
             t.join()
         assert errs == []
+
+
+POOL_SCRIPT = r"""
+import ctypes, sys, threading
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import lstore_amd as L
+import oracle as O
+lib = L.lib()
+lib.lsec_test_staging_pool.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_longlong)]
+k, m, C, n = 6, 3, 1 << 20, 32  # 288 MiB contiguous: pinned in place, slots of ~252 MiB of HBM
+errors = []
+plan = L.Plan.for_chunk(L.REED_SOL_VAN, k, m, C)
+bar = threading.Barrier(8)
+
+
+def worker(t):
+    try:
+        st = np.zeros((n, k + m, C), np.uint8)
+        st[:, :k] = np.random.default_rng(t).integers(0, 256, (n, k, C), dtype=np.uint8)
+        bar.wait()
+        for _ in range(2):
+            plan.encode_stripes(st)
+        for s in (0, n - 1):
+            if not np.array_equal(st[s, k:], O.encode(L.REED_SOL_VAN, st[s, :k], m, 0)):
+                errors.append((t, s))
+    except Exception as e:
+        errors.append((t, repr(e)))
+
+
+th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+for x in th:
+    x.start()
+for x in th:
+    x.join()
+out = (ctypes.c_longlong * 3)()
+lib.lsec_test_staging_pool(0, out)
+print(list(out), errors)
+assert not errors, errors
+assert out[0] >= 3 and out[1] <= 2, list(out)  # several pipelines ran; at most 2 keep the large halves
+assert out[2] <= 2 * 3 * (300 << 20) + out[0] * 3 * (64 << 20), list(out)
+print("ok")
+"""
+
+
+def test_staging_pool_keeps_at_most_two_large_device_halves(cuda):
+    """Eight threads of large pageable batches (pinned in place, so their slots take the large
+    device geometry, LSEC_DEV_STAGING_MB): afterwards at most two pooled pipelines keep their
+    large device halves, so the HBM the pool holds does not grow with the peak thread count
+    (ADVICE r05); every batch's parity bit-exact."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", POOL_SCRIPT, root], capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), (out.stdout[-800:], out.stderr[-1500:])

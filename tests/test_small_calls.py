@@ -158,7 +158,14 @@ REF = os.path.join(ROOT, "oracle", "_ref", "libjerasure_ref.so")
 @pytest.mark.parametrize("chunk,threads,method,op,pinned,extra", [
     (16384, 128, "reed_sol_van", "encode", 0, {}), (16384, 128, "cauchy_good", "decode", 0, {}),
     (65536, 64, "cauchy_good", "encode", 1, {}), (1 << 20, 16, "reed_sol_van", "encode", 0, {}),
-    (262144, 32, "reed_sol_van", "decode", 0, {"LSEC_ZC_SLOTS_MB": "4"})])
+    (262144, 32, "reed_sol_van", "decode", 0, {"LSEC_ZC_SLOTS_MB": "4"}),
+    # LStore's buffer lifetime: each call's parity / stripe buffer malloc'd for the call and freed
+    # right after it (segment/jerasure.c:1689-1697, :1882, :1621); =2 makes every buffer a fresh
+    # mmap and every free an munmap, so the next buffer reuses just-unmapped addresses
+    (1 << 20, 2, "reed_sol_van", "encode", 0, {"FNPTR_FREE_AFTER": "2"}),
+    (1 << 20, 4, "cauchy_good", "decode", 0, {"FNPTR_FREE_AFTER": "2"}),
+    (1 << 20, 3, "cauchy_good", "decode", 0, {"FNPTR_FREE_AFTER": "1"}),
+    (4 << 20, 2, "reed_sol_van", "encode", 0, {"FNPTR_FREE_AFTER": "1"})])
 def test_fn_pointer_stress_bit_exact(cuda, chunk, threads, method, op, pinned, extra):
     """LStore's pattern in C (tools/fnptr_bench.c, FNPTR_VERIFY=1): every thread calls
     encode_block / decode_block on its own stripe for 1 s; before each call the chunks it must
@@ -340,10 +347,153 @@ print("ok", len(arenas))
 
 
 def test_background_unpinner_and_drain(cuda):
-    """Three threads of per-stripe 1 MiB calls on fresh pageable stripes (pinned in place; with
-    other calls in flight, each call's registration is dropped by the background unpinner after it
-    returns, ec_pinning.cpp): every result equals the oracle's, and after lsec_host_unpin_drain()
-    the caller can register and release those ranges itself (INTEGRATION.md "Host buffers")."""
-    out = subprocess.run([sys.executable, "-c", UNPIN_SCRIPT, ROOT], capture_output=True, text=True, timeout=110)
+    """The opt-in background unpinner (LSEC_DEFER_UNPIN_MB > 0; off by default).  Three threads of
+    per-stripe 1 MiB calls on fresh pageable stripes (pinned in place; with other calls in flight,
+    each call's registration is dropped by the background unpinner after it returns,
+    ec_pinning.cpp): every result equals the oracle's, and after lsec_host_unpin_drain() the caller
+    can register and release those ranges itself (INTEGRATION.md "Host buffers")."""
+    out = subprocess.run([sys.executable, "-c", UNPIN_SCRIPT, ROOT], capture_output=True, text=True, timeout=110,
+                         env=dict(os.environ, LSEC_DEFER_UNPIN_MB="256"))
     assert out.returncode == 0, (out.stdout[-500:], out.stderr[-1500:])
     assert out.stdout.strip().startswith("ok"), out.stdout[-300:]
+
+
+FREE_AFTER_SCRIPT = r"""
+import ctypes, json, sys, threading
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+mode = sys.argv[2]
+import torch
+import lstore_amd as L
+import oracle as O
+hip = ctypes.CDLL("libamdhip64.so")
+libc = ctypes.CDLL(None, use_errno=True)
+libc.mmap.restype = ctypes.c_void_p
+libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+PROT_RW, MAP_PRIVATE_ANON, MAP_FIXED_NOREPLACE = 0x3, 0x22, 0x100000
+MAP_FAILED = ctypes.c_void_p(-1).value
+
+
+class Attr(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int), ("device", ctypes.c_int), ("devicePointer", ctypes.c_void_p),
+                ("hostPointer", ctypes.c_void_p), ("isManaged", ctypes.c_int), ("allocationFlags", ctypes.c_uint)]
+
+
+hip.hipPointerGetAttributes.argtypes = [ctypes.POINTER(Attr), ctypes.c_void_p]
+hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+
+
+def registered(addr, n):
+    # page-locked with HIP at either end of [addr, addr + n)?  (a failed query leaves an error in
+    # this thread's last-error slot: read it, so torch's next launch check does not take it)
+    for a in (addr, addr + n - 1):
+        at = Attr()
+        rc = hip.hipPointerGetAttributes(ctypes.byref(at), ctypes.c_void_p(a))
+        if rc != 0:
+            hip.hipGetLastError()
+        elif at.type != 0:
+            return True
+    return False
+
+
+def fresh(n, hint=None):
+    p = libc.mmap(hint, n, PROT_RW, MAP_PRIVATE_ANON | (MAP_FIXED_NOREPLACE if hint else 0), -1, 0)
+    return None if p in (None, MAP_FAILED) else p
+
+
+def view(addr, n):
+    return np.frombuffer((ctypes.c_uint8 * n).from_address(addr), dtype=np.uint8)
+
+
+k, m, C = 6, 3, 1 << 20
+S = (k + m) * C
+plan = L.Plan.for_chunk(L.REED_SOL_VAN, k, m, C)
+plan.prepare_encode()
+plan.prepare_decode([0])
+dev = torch.empty(S, dtype=torch.uint8, device="cuda")
+stats = dict(calls=0, still_registered=0, reused_address=0, copies_checked=0, bad=[])
+lock = threading.Lock()
+
+
+def worker(t):
+    rng = np.random.default_rng(100 + t)
+    devt = torch.empty(S, dtype=torch.uint8, device="cuda")
+    try:
+        for it in range(24):
+            a = fresh(S)
+            d = view(a, S).reshape(k + m, C)
+            d[:k] = rng.integers(0, 256, (k, C), dtype=np.uint8)
+            want_p = O.encode(L.REED_SOL_VAN, np.ascontiguousarray(d[:k]), m, plan.packet_size)
+            plan.encode_block([d[j] for j in range(k + m)])
+            reg = registered(a, S)  # right after the call returned, other threads' calls in flight
+            ok = np.array_equal(d[k:], want_p)
+            want0 = d[0].copy()
+            d[0] = 0
+            plan.decode_block([d[j] for j in range(k + m)], [0])
+            reg = registered(a, S) or reg
+            ok = ok and np.array_equal(d[0], want0)
+            with lock:
+                stats["calls"] += 2
+                stats["still_registered"] += int(reg)
+                if not ok:
+                    stats["bad"].append((t, it, "coding"))
+            if mode == "optin":
+                # count only: with the opt-in a registration may still be pending here, and a copy
+                # from a recycled range under it is the hazard the default avoids
+                libc.munmap(a, S)
+                continue
+            # LStore's pattern: free the buffer right after the op (segment/jerasure.c:1882), and
+            # the next allocation lands at the same addresses
+            libc.munmap(a, S)
+            b = fresh(S, a) or fresh(S)
+            with lock:
+                stats["reused_address"] += int(b == a)
+            y = view(b, S)
+            y[:] = rng.integers(0, 256, S, dtype=np.uint8)
+            # another HIP user of the process copies the new buffer: torch, and a plain hipMemcpy
+            got = torch.from_numpy(y).cuda().cpu().numpy()
+            good = np.array_equal(got, y)
+            if hip.hipMemcpy(ctypes.c_void_p(devt.data_ptr()), ctypes.c_void_p(b), S, 1) != 0:
+                good = False
+            good = good and np.array_equal(devt.cpu().numpy(), y)
+            with lock:
+                stats["copies_checked"] += 2
+                if not good:
+                    stats["bad"].append((t, it, "copy of a recycled range", b == a))
+            libc.munmap(b, S)
+    except Exception as e:
+        with lock:
+            stats["bad"].append((t, repr(e)))
+
+
+th = [threading.Thread(target=worker, args=(t,)) for t in range(3)]
+for x in th:
+    x.start()
+for x in th:
+    x.join()
+print(json.dumps(stats))
+"""
+
+
+def _free_after(mode, extra_env=None):
+    env = dict(os.environ, **(extra_env or {}))
+    out = subprocess.run([sys.executable, "-c", FREE_AFTER_SCRIPT, ROOT, mode], capture_output=True, text=True,
+                         timeout=110, env=env)
+    assert out.returncode == 0, (out.stdout[-500:], out.stderr[-1500:])
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_no_registration_outlives_its_call(cuda):
+    """LStore frees a call's buffers right after the op (the parity buffer, segment/jerasure.c:1689-1697
+    and :1882; the read path's stripe buffer, :1621), and the allocator may hand the same addresses
+    out again at once.  Three threads of 1 MiB per-stripe calls on freshly mmap'd stripes (pinned in
+    place for the call), each munmap'd right after its call, with the next mmap asked for the same
+    addresses; another HIP user of the process (torch's .cuda(), a plain hipMemcpy) then copies the
+    new bytes.  With the default (LSEC_DEFER_UNPIN_MB=0) no range the engine registered is still
+    registered when its call returns -- even while the other threads' calls are in flight -- so the
+    copies see the new pages; every coding result is bit-exact."""
+    st = _free_after("default", {"LSEC_DEFER_UNPIN_MB": "0"})
+    assert st["calls"] == 144 and not st["bad"], st
+    assert st["still_registered"] == 0, st
+    assert st["copies_checked"] == 144 and st["reused_address"] > 0, st

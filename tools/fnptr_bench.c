@@ -29,9 +29,20 @@
  *                        are overwritten before the call, and after it must equal the reference's
  *                        (parity for encode, the lost data chunk 0 for decode); the JSON line then
  *                        carries "verified" and "mismatches", and the exit status is 2 on any
+ *        FNPTR_FREE_AFTER=1  LStore's buffer lifetime: every encode writes its parity into a buffer
+ *                        malloc'd for that call and freed right after it (segjerase_write_func:
+ *                        segment/jerasure.c:1689-1697, free at :1882); every decode works on a stripe
+ *                        buffer malloc'd for the call, filled from the thread's stripes (the bytes
+ *                        the depots returned) and freed after it (the read path, :1621).
+ *                        =2: the same with glibc's mmap threshold fixed at 128 KiB (mallopt), so
+ *                        every buffer is a fresh mmap and every free an munmap: the next call's
+ *                        buffer often lands at the addresses just unmapped, the case a
+ *                        registration outliving its call would get wrong.  With FNPTR_VERIFY every
+ *                        call's output is checked before the free.
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
+#include <malloc.h>
 #include <sched.h>
 #include <pthread.h>
 #include <sys/resource.h>
@@ -50,7 +61,7 @@ static void (*g_ref_encode)(void *, char **, int);
 static int (*g_ref_decode)(void *, char **, int, int *);
 static int (*g_host_malloc)(void **, size_t, unsigned);
 static int (*g_host_free)(void *);
-static int g_chunk, g_decode, g_use_ref, g_verify, g_k = 6, g_m = 3;
+static int g_chunk, g_decode, g_use_ref, g_verify, g_free_after, g_k = 6, g_m = 3;
 static long g_nbuf = 1;  /* stripes per thread (FNPTR_SET_MB) */
 static double g_set_mb;
 static long g_verified, g_mismatch;  /* FNPTR_VERIFY counters (atomic adds) */
@@ -122,14 +133,39 @@ static void *worker(void *arg)
             if (g_decode) memset(ptr[0], 0xA5, C);
             else memset(ptr[k], 0x5A, (size_t)m * C);
         }
+        char *own = NULL;  /* FNPTR_FREE_AFTER: this call's buffer, freed after the call */
+        char *cptr[256];
+        char **p = ptr;
+        if (g_free_after) {
+            memcpy(cptr, ptr, sizeof(char *) * (size_t)(k + m));
+            if (g_decode) {  /* the stripe as read from the depots, into a buffer of its own */
+                own = malloc((size_t)(k + m) * C);
+                if (own) {
+                    for (int i = 0; i < k + m; i++) {
+                        cptr[i] = own + (size_t)i * C;
+                        memcpy(cptr[i], ptr[i], C);
+                    }
+                    memset(cptr[0], 0xA5, C);
+                }
+            } else {  /* the parity buffer of one write op */
+                own = malloc((size_t)m * C);
+                if (own) {
+                    for (int r2 = 0; r2 < m; r2++) cptr[k + r2] = own + (size_t)r2 * C;
+                    memset(own, 0x5A, (size_t)m * C);
+                }
+            }
+            if (!own) break;
+            p = cptr;
+        }
         double t0 = now();
-        one_call(ptr, erasures);
+        one_call(p, erasures);
         double t1 = now();
         if (gold) {
-            const int bad = g_decode ? memcmp(ptr[0], gold, C) != 0 : memcmp(ptr[k], gold + (size_t)k * C, (size_t)m * C) != 0;
+            const int bad = g_decode ? memcmp(p[0], gold, C) != 0 : memcmp(p[k], gold + (size_t)k * C, (size_t)m * C) != 0;
             __atomic_add_fetch(&g_verified, 1, __ATOMIC_RELAXED);
             if (bad) __atomic_add_fetch(&g_mismatch, 1, __ATOMIC_RELAXED);
         }
+        free(own);
         if (r->nlat < MAX_SAMPLES) r->lat[r->nlat++] = t1 - t0;
         r->calls++;
         if (t1 >= g_t_end) break;
@@ -244,12 +280,12 @@ static void run(int T, const char *impl, const char *method)
            "\"method\": \"%s\", \"pinned\": %d, \"per_call_us_p50\": %.1f, "
            "\"per_call_us_p99\": %.1f, \"per_call_us_p999\": %.1f, \"per_call_us_max\": %.1f, \"per_call_us_mean\": %.1f, "
            "\"gibps\": %.3f, \"cpu_util\": %.2f, \"cpu_us_per_call\": %.1f, \"cgroup_throttled_ms\": %.1f, "
-           "\"verified\": %ld, \"mismatches\": %ld, \"stripes_per_thread\": %ld, \"set_mib\": %.0f}\n",
+           "\"verified\": %ld, \"mismatches\": %ld, \"stripes_per_thread\": %ld, \"set_mib\": %.0f, \"free_after\": %d}\n",
            impl, g_decode ? "decode" : "encode", g_chunk, T, calls, wall, method, g_host_malloc != NULL,
            n ? lat[n / 2] * 1e6 : 0.0, n ? lat[(size_t)(n * 0.99)] * 1e6 : 0.0, n ? lat[(size_t)(n * 0.999)] * 1e6 : 0.0,
            n ? lat[n - 1] * 1e6 : 0.0, n ? sum / n * 1e6 : 0.0, calls * (double)g_k * g_chunk / wall / (1 << 30),
            cpu / wall, calls ? cpu / calls * 1e6 : 0.0, thr * 1e3, g_verified, g_mismatch, g_nbuf,
-           g_nbuf * (double)T * stripe / (1 << 20));
+           g_nbuf * (double)T * stripe / (1 << 20), g_free_after);
     fflush(stdout);
     free(lat);
 }
@@ -284,6 +320,8 @@ int main(int argc, char **argv)
     const char *only_ref = getenv("FNPTR_ONLY_REF");
     const char *ref_so = getenv("FNPTR_REF");
     g_verify = getenv("FNPTR_VERIFY") && atoi(getenv("FNPTR_VERIFY"));
+    g_free_after = getenv("FNPTR_FREE_AFTER") ? atoi(getenv("FNPTR_FREE_AFTER")) : 0;
+    if (g_free_after == 2) mallopt(M_MMAP_THRESHOLD, 128 * 1024);  /* fixed: every buffer is mmap'd */
     if (ref_so && *ref_so) {
         void *h = dlopen(ref_so, RTLD_NOW | RTLD_LOCAL);
         void *(*ref_new)(int, int, int, int, int) = h ? (void *(*)(int, int, int, int, int))dlsym(h, "ref_plan_new") : NULL;

@@ -21,12 +21,12 @@ for s in $steps; do
         || { echo "bench failed"; tail -20 "gpurun_out/bench_${tag}.log"; exit 1; }
       echo "bench ok" ;;
     ranks)
-      timeout -k 10 300 python bench.py --gpus 2 --share-gpus --stripes 512 --steps 10 --no-pmc --json-out "gpurun_out/bench2_${tag}.json" \
+      timeout -k 10 300 python bench.py --gpus 2 --share-gpus --steps 10 --json-out "gpurun_out/bench2_${tag}.json" \
         > "gpurun_out/bench2_${tag}.log" 2>&1 || { echo "2-rank bench failed"; tail -20 "gpurun_out/bench2_${tag}.log"; exit 1; }
       echo "2-rank ok" ;;
     c4)
       timeout -k 10 300 python bench.py --method cauchy_good --k 10 --m 4 --chunk 4194304 --total-stripes 2048 --gpus 2 --share-gpus \
-        --steps 10 --no-pmc --json-out "gpurun_out/c4_2rank_${tag}.json" > "gpurun_out/c4_2rank_${tag}.log" 2>&1 \
+        --steps 10 --json-out "gpurun_out/c4_2rank_${tag}.json" > "gpurun_out/c4_2rank_${tag}.log" 2>&1 \
         || { echo "c4 2-rank failed"; tail -20 "gpurun_out/c4_2rank_${tag}.log"; exit 1; }
       echo "c4 2-rank ok" ;;
   esac
