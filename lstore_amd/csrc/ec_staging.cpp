@@ -233,6 +233,7 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
   const bool aligned = kpol != KernelCopy::kNever && kernel_transport_aligned(ptrs, nstripes, km, in_ids, out_ids, C, cb);
   CallerPinned cp = caller_pinned(ptrs, nstripes, km, in_ids, out_ids, C, aligned);
   const bool caller_pinned = cp.pinned;
+  const auto t_reg0 = now();
   const RouteTable &rt = routes();
   const bool pinned = caller_pinned || inplace.pin(ptrs, nstripes, km, in_ids, out_ids, C,
                                                    eager_pin ? rt.own_dma_min_bytes : rt.pin_min_bytes,
@@ -418,9 +419,10 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
     const auto t_rel0 = now();
     inplace.release();  // (the destructor would, after this print)
     const auto t_end = now();
-    fprintf(stderr, "[lsec trace] host call %d stripes, %d in / %d out x %lld B (%s): pin %.2f ms, submit %.2f ms, "
-                    "drain %.2f ms, unpin %.2f ms\n",
+    fprintf(stderr, "[lsec trace] host call %d stripes, %d in / %d out x %lld B (%s): pin %.4f ms (query %.4f, register %.4f), "
+                    "submit %.4f ms, drain %.4f ms, unpin %.4f ms\n",
             nstripes, nin, nout, C, by_kernel ? "kernel transport" : pinned ? "pinned DMA" : "packed", ms(t_pin0, t_loop0),
+            ms(t_pin0, t_reg0), ms(t_reg0, t_loop0),
             ms(t_loop0, t_drain0), ms(t_drain0, t_rel0), ms(t_rel0, t_end));
   }
   if (dacc) {

@@ -29,6 +29,8 @@
  *                        are overwritten before the call, and after it must equal the reference's
  *                        (parity for encode, the lost data chunk 0 for decode); the JSON line then
  *                        carries "verified" and "mismatches", and the exit status is 2 on any
+ *        FNPTR_LAT_OUT=path  every timed call's latency (us), one line per call in call order
+ *                        ("thread latency"), for joining with LSEC_TRACE's per-call phases
  *        FNPTR_FREE_AFTER=1  LStore's buffer lifetime: every encode writes its parity into a buffer
  *                        malloc'd for that call and freed right after it (segjerase_write_func:
  *                        segment/jerasure.c:1689-1697, free at :1882); every decode works on a stripe
@@ -264,6 +266,15 @@ static void run(int T, const char *impl, const char *method)
         pthread_join(th[t], NULL);
         calls += rec[t].calls;
         n += rec[t].nlat;
+    }
+    const char *lat_out = getenv("FNPTR_LAT_OUT");
+    if (lat_out && *lat_out) {  /* in call order, before the sort */
+        FILE *f = fopen(lat_out, "w");
+        if (f) {
+            for (int t = 0; t < T; t++)
+                for (long i = 0; i < rec[t].nlat; i++) fprintf(f, "%d %.2f\n", t, rec[t].lat[i] * 1e6);
+            fclose(f);
+        }
     }
     double *lat = malloc(sizeof(double) * (n ? n : 1));
     long o = 0;
