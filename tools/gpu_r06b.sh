@@ -24,6 +24,22 @@ for s in $steps; do
       python -c "
 import json; rs=[json.loads(l) for l in open('$o')]
 print('free-after verified calls', sum(r['verified'] for r in rs), 'mismatches', sum(r['mismatches'] for r in rs))" ;;
+    churn)  # FNPTR_FREE_AFTER=2 (a fresh mmap per call): the engine's phases, the engine with no in-place
+            # registration, and the reference, one thread and two
+      o=gpurun_out/free_after_churn_${tag}.jsonl; : > $o
+      for th in 1 2; do
+        for e in "X=0" "LSEC_NO_HOST_REGISTER=1" "LSEC_OWN_DMA_MAX=0"; do
+          env $e FNPTR_REF=$REF FNPTR_FREE_AFTER=2 timeout -k 10 60 build/fnptr_bench 1048576 $th 2 cauchy_good decode \
+            | sed "s/}\$/, \"env\": \"$e\"}/" >> $o || { echo "churn run failed: $e"; exit 1; }
+        done
+      done
+      LSEC_TRACE=1 FNPTR_FREE_AFTER=2 timeout -k 10 60 build/fnptr_bench 1048576 1 1 cauchy_good decode \
+        > gpurun_out/free_after_churn_trace_${tag}.json 2> gpurun_out/free_after_churn_trace_${tag}.txt || { echo "traced churn failed"; exit 1; }
+      python -c "
+import json
+for l in open('$o'):
+    r = json.loads(l); print(r['impl'], r['threads'], r['env'], r['per_call_us_p50'], r['gibps'])"
+      grep "lsec trace" gpurun_out/free_after_churn_trace_${tag}.txt | tail -3 ;;
     probe)
       timeout -k 10 240 python tools/probes/free_after_probe.py > gpurun_out/free_after_probe_${tag}.jsonl \
         || { echo "probe failed"; cat gpurun_out/free_after_probe_${tag}.jsonl; exit 1; }
