@@ -375,6 +375,14 @@ extern std::atomic<unsigned long long> g_st_srv_timeouts;
 // server, refused by it (no free slots: claim failed, or not servable), then run as their own
 // launch (kernel over the caller's page-locked chunks, or over this thread's slot)
 extern thread_local std::chrono::steady_clock::time_point tl_call_t0;  // fn-pointer entry (LSEC_STATS)
+// LSEC_TRACE of a fn-pointer call: run_host leaves its phase line here (line[0] != 0) instead of
+// printing it, and the fn-pointer prints it with the time before run_host (entry) and after it (exit)
+struct CallTrace {
+  bool active = false;
+  std::chrono::steady_clock::time_point t_call0, t_run0, t_run1;
+  char line[320] = {0};
+};
+extern thread_local CallTrace tl_trace;
 extern thread_local std::chrono::steady_clock::time_point tl_zc_t0;    // run_zerocopy entry (LSEC_STATS)
 extern thread_local long long tl_call_cpu0, tl_zc_cpu0;           // this thread's CPU ns at both
 

@@ -84,10 +84,7 @@ hipError_t by_r(int R, F f) {
 //                                                            RS 20+6 67 %, 16+4 79 % vs 51 / 63 %
 //   otherwise                                                2 x 16 B per lane, branch-free
 int bytewise_shape(int K, int R) {
-  if (g_bw_variant > 0) {
-    const int shape = (g_bw_variant - 1) % kBwShapes;
-    return shape >= 5 && R != 1 ? 0 : shape;  // (shapes 5 / 6 exist for single-output launches only)
-  }
+  if (g_bw_variant > 0) return (g_bw_variant - 1) % kBwShapes;
   if (R == 1) return 4;
   return K >= 16 ? 1 : 0;
 }

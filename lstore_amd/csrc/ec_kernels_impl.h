@@ -1078,11 +1078,9 @@ hipError_t bytewise_k(const ApplyArgs &a, hipStream_t st, int grid) {
 //   2 -> (2, 2) 16 B/lane in 8 B pieces, branch-free   3 -> (1, 2) 8 B/lane, branch-free
 //   4 -> (1, 2) 8 B/lane, per-cell branches (single-output decodes: mostly XORs of
 //        coefficient-1 inputs, which the branch turns into one v_xor instead of 3 perms)
-//   5 -> (1, 4) 16 B/lane, per-cell branches; 6 -> (2, 4) 32 B/lane, per-cell branches
-//        (single-output launches only: R = 1; other R take shape 0)
-constexpr int kBwShapes = 7;
-inline int bw_shape_it(int shape) { return (shape == 0 || shape == 2 || shape == 6) ? 2 : 1; }
-inline int bw_shape_vw(int shape) { return shape <= 1 || shape >= 5 ? 4 : 2; }
+constexpr int kBwShapes = 5;
+inline int bw_shape_it(int shape) { return (shape == 0 || shape == 2) ? 2 : 1; }
+inline int bw_shape_vw(int shape) { return shape <= 1 ? 4 : 2; }
 
 template <int R>
 hipError_t dispatch_bytewise(const ApplyArgs &a, hipStream_t st, int grid, int shape) {
@@ -1094,12 +1092,6 @@ hipError_t dispatch_bytewise(const ApplyArgs &a, hipStream_t st, int grid, int s
     case 2: return bytewise_k<R, 2, true, 2>(a, st, grid);
     case 3: return bytewise_k<R, 1, true, 2>(a, st, grid);
     case 4: return bytewise_k<R, 1, false, 2>(a, st, grid);
-    case 5:
-      if constexpr (R == 1) return bytewise_k<R, 1, false, 4>(a, st, grid);
-      else return bytewise_k<R, 2, true, 4>(a, st, grid);
-    case 6:
-      if constexpr (R == 1) return bytewise_k<R, 2, false, 4>(a, st, grid);
-      else return bytewise_k<R, 2, true, 4>(a, st, grid);
     default: return bytewise_k<R, 2, true, 4>(a, st, grid);
   }
 }

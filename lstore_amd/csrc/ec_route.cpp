@@ -462,7 +462,41 @@ int retry_direct(PlanExt *e, char **ptr, long long C, const std::vector<int> &id
   return -1;
 }
 
+thread_local CallTrace tl_trace;
+
+namespace {
+bool call_trace_on() {
+  static const bool on = getenv("LSEC_TRACE") != nullptr;
+  return on;
+}
+void call_trace_begin() {
+  tl_trace.active = true;
+  tl_trace.line[0] = 0;
+  tl_trace.t_call0 = std::chrono::steady_clock::now();
+}
+// the call's run_host phases (if it took route 4) with the time spent before run_host began
+// (entry: pointer queries, decode image lookup, routing, staging acquisition) and after it ended
+// (exit: staging release, return)
+void call_trace_end() {
+  const auto t = std::chrono::steady_clock::now();
+  const auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  };
+  if (tl_trace.line[0])
+    fprintf(stderr, "%s, entry %.4f ms, exit %.4f ms, call %.4f ms\n", tl_trace.line, ms(tl_trace.t_call0, tl_trace.t_run0),
+            ms(tl_trace.t_run1, t), ms(tl_trace.t_call0, t));
+  tl_trace.active = false;
+  tl_trace.line[0] = 0;
+}
+}  // namespace
+
 void fp_encode_block(lio_erasure_plan_t *p, char **ptr, int block_size) {
+  if (call_trace_on()) call_trace_begin();
+  struct End {
+    ~End() {
+      if (tl_trace.active) call_trace_end();
+    }
+  } end_trace;
   if (ZcStats::on()) {
     tl_call_t0 = std::chrono::steady_clock::now();
     tl_call_cpu0 = thread_cpu_ns();
@@ -480,6 +514,12 @@ void fp_encode_block(lio_erasure_plan_t *p, char **ptr, int block_size) {
 }
 
 int fp_decode_block(lio_erasure_plan_t *p, char **ptr, int block_size, int *erasures) {
+  if (call_trace_on()) call_trace_begin();
+  struct End {
+    ~End() {
+      if (tl_trace.active) call_trace_end();
+    }
+  } end_trace;
   if (ZcStats::on()) {
     tl_call_t0 = std::chrono::steady_clock::now();
     tl_call_cpu0 = thread_cpu_ns();

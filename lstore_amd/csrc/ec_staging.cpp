@@ -419,11 +419,19 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
     const auto t_rel0 = now();
     inplace.release();  // (the destructor would, after this print)
     const auto t_end = now();
-    fprintf(stderr, "[lsec trace] host call %d stripes, %d in / %d out x %lld B (%s): pin %.4f ms (query %.4f, register %.4f), "
-                    "submit %.4f ms, drain %.4f ms, unpin %.4f ms\n",
+    char line[320];
+    snprintf(line, sizeof(line), "[lsec trace] host call %d stripes, %d in / %d out x %lld B (%s): pin %.4f ms (query %.4f, register %.4f), "
+                    "submit %.4f ms, drain %.4f ms, unpin %.4f ms",
             nstripes, nin, nout, C, by_kernel ? "kernel transport" : pinned ? "pinned DMA" : "packed", ms(t_pin0, t_loop0),
             ms(t_pin0, t_reg0), ms(t_reg0, t_loop0),
             ms(t_loop0, t_drain0), ms(t_drain0, t_rel0), ms(t_rel0, t_end));
+    if (tl_trace.active) {  // a fn-pointer call: it prints the line with its entry and exit times
+      memcpy(tl_trace.line, line, sizeof(line));
+      tl_trace.t_run0 = t_pin0;
+      tl_trace.t_run1 = t_end;
+    } else {
+      fprintf(stderr, "%s\n", line);
+    }
   }
   if (dacc) {
     if (hipStreamSynchronize(stg->s_out) != hipSuccess && !rc) rc = fail("magic sync failed");

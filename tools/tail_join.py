@@ -6,8 +6,10 @@ per-call phases (LSEC_TRACE=1 on stderr) and say what the slowest calls spend th
 
 At one thread every call is one route-4 host call, so the last N trace lines of the matching shape
 are the N timed calls, in order (the warm-up calls come first).  Prints one JSON line per group
-(the slowest `tail` fraction, the rest): latency, each phase's mean, how many calls paid a
-registration miss (register > 50 us), and the part of the latency outside the traced phases.
+(the slowest `tail` fraction, the rest): latency, each phase's mean (entry / exit: the fn-pointer
+call's time before run_host began and after it ended; call: the whole call as the engine saw it), how
+many calls paid a registration miss (register > 50 us), and the part of the caller's latency outside
+every traced phase (the call's own entry and return, and the trace print itself).
 """
 import argparse
 import json
@@ -15,7 +17,7 @@ import re
 import sys
 
 PHASE = re.compile(r"pin ([\d.]+) ms \(query ([\d.]+), register ([\d.]+)\), submit ([\d.]+) ms, drain ([\d.]+) ms, "
-                   r"unpin ([\d.]+) ms")
+                   r"unpin ([\d.]+) ms(?:, entry ([\d.]+) ms, exit ([\d.]+) ms, call ([\d.]+) ms)?")
 
 
 def main():
@@ -32,7 +34,7 @@ def main():
             if "[lsec trace] host call" in line and a.match in line:
                 m = PHASE.search(line)
                 if m:
-                    phases.append([float(x) * 1e3 for x in m.groups()])  # us
+                    phases.append([float(x) * 1e3 if x is not None else 0.0 for x in m.groups()])  # us
     lats = []
     with open(a.lat) as f:
         for line in f:
@@ -44,7 +46,7 @@ def main():
     rows = list(zip(lats, phases[len(phases) - len(lats):]))
     rows.sort(key=lambda r: r[0])
     cut = max(1, int(round(len(rows) * a.tail)))
-    names = ("pin", "query", "register", "submit", "drain", "unpin")
+    names = ("pin", "query", "register", "submit", "drain", "unpin", "entry", "exit", "call")
     lat_sorted = [r[0] for r in rows]
 
     def pct(p):
@@ -56,7 +58,7 @@ def main():
     for label, grp in (("slowest %g" % a.tail, rows[-cut:]), ("rest", rows[:-cut])):
         n = len(grp)
         mean = [sum(r[1][i] for r in grp) / n for i in range(len(names))]
-        outside = sum(r[0] - (r[1][0] + r[1][3] + r[1][4] + r[1][5]) for r in grp) / n
+        outside = sum(r[0] - (r[1][0] + r[1][3] + r[1][4] + r[1][5] + r[1][6] + r[1][7]) for r in grp) / n
         print(json.dumps({"group": label, "calls": n, "latency_mean_us": round(sum(r[0] for r in grp) / n, 1),
                           **{f"{nm}_mean_us": round(v, 1) for nm, v in zip(names, mean)},
                           "outside_phases_mean_us": round(outside, 1),
