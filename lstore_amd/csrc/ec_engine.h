@@ -301,6 +301,16 @@ class InPlacePin {
 // calls holding in-place registrations at this moment (this one included when it holds some)
 int in_place_calls();
 
+// The in-place stall guard.  DMA from pages pinned in place can stall for tens of milliseconds when
+// the process keeps unmapping and remapping host memory while calls run (round 6: per-stripe
+// calls on buffers that are each a fresh mmap, munmapped after the call, at two threads: ~25 ms per
+// call in the drain against ~0.3 ms packed; profiles/r06_v2_free_after_churn.jsonl).  run_host
+// reports every pinned call's drain; three stalls (under 1 GB/s and over 5 ms) within 64 calls
+// suspend in-place pinning -- calls pack into the engine's page-locked staging instead -- for 30 s,
+// doubling on every recurrence up to 10 min.  LSEC_INPLACE_GUARD=0 turns the guard off.
+void note_inplace_drain(size_t bytes, double drain_ms);
+bool inplace_suspended();
+
 // DMA runs: pieces whose source and destination both continue the previous piece merge
 // into one copy (LStore's k data chunks of a stripe sit back to back in one cache page, so
 // a stripe's inputs usually become a single k*C transfer)

@@ -231,9 +231,56 @@ CallerPinned caller_pinned(char **ptrs, int nstripes, int km, const std::vector<
   return r;
 }
 
+namespace {
+std::atomic<int> g_guard_calls{0}, g_guard_stalls{0}, g_guard_level{0};
+std::atomic<long long> g_guard_until_ns{0};
+std::mutex g_guard_mu;
+
+long long steady_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+bool guard_on() {
+  static const bool on = [] {
+    const char *e = getenv("LSEC_INPLACE_GUARD");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+}  // namespace
+
+bool inplace_suspended() {
+  if (!guard_on()) return false;
+  const long long until = g_guard_until_ns.load(std::memory_order_relaxed);
+  return until != 0 && steady_ns() < until;
+}
+
+void note_inplace_drain(size_t bytes, double drain_ms) {
+  if (!guard_on()) return;
+  const bool stall = drain_ms > 5.0 && static_cast<double>(bytes) / (drain_ms * 1e-3) < 1e9;
+  const int calls = g_guard_calls.fetch_add(1, std::memory_order_relaxed) + 1;
+  const int stalls = stall ? g_guard_stalls.fetch_add(1, std::memory_order_relaxed) + 1 : g_guard_stalls.load(std::memory_order_relaxed);
+  if (stalls >= 3) {
+    std::lock_guard<std::mutex> lk(g_guard_mu);
+    if (g_guard_stalls.load(std::memory_order_relaxed) < 3) return;  // another thread suspended just now
+    const int level = std::min(g_guard_level.fetch_add(1, std::memory_order_relaxed), 4);
+    const long long secs = 30LL << level;  // 30 s, 60, 120, 240, 480 (10 min cap below)
+    const long long s2 = std::min(secs, 600LL);
+    g_guard_until_ns.store(steady_ns() + s2 * 1000000000LL, std::memory_order_relaxed);
+    g_guard_calls.store(0, std::memory_order_relaxed);
+    g_guard_stalls.store(0, std::memory_order_relaxed);
+    fprintf(stderr, "liblstore_ec: DMA from host pages pinned in place stalled (%.1f ms for %zu B); pinning in place "
+                    "suspended for %lld s, calls pack into page-locked staging (LSEC_INPLACE_GUARD=0 turns this off)\n",
+            drain_ms, bytes, s2);
+  } else if (calls >= 64) {  // a fresh window
+    g_guard_calls.store(0, std::memory_order_relaxed);
+    g_guard_stalls.store(0, std::memory_order_relaxed);
+  }
+}
+
 bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &in_ids, const std::vector<int> &out_ids,
                      long long C, size_t min_bytes, size_t min_run) {
-  if (!routes().pin_in_place) return false;
+  if (!routes().pin_in_place || inplace_suspended()) return false;
   std::vector<std::pair<char *, char *>> pieces;
   pieces.reserve(static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()));
   for (int s = 0; s < nstripes; ++s) {

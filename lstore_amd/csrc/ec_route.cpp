@@ -469,6 +469,22 @@ bool call_trace_on() {
   static const bool on = getenv("LSEC_TRACE") != nullptr;
   return on;
 }
+// LSEC_TRACE=2: the lines are kept in memory and printed at exit, so that no write to stderr
+// sits between one call and the next (the one-thread tail study, tools/gpu_fnptr_tail.sh)
+bool call_trace_buffered() {
+  static const bool b = [] {
+    const char *e = getenv("LSEC_TRACE");
+    return e && std::strcmp(e, "2") == 0;
+  }();
+  return b;
+}
+std::mutex g_trace_mu;
+std::vector<std::string> *g_trace_lines = nullptr;  // leaked: printed by the exit handler
+void print_trace_lines() {
+  std::lock_guard<std::mutex> lk(g_trace_mu);
+  if (g_trace_lines)
+    for (const std::string &l : *g_trace_lines) fprintf(stderr, "%s\n", l.c_str());
+}
 void call_trace_begin() {
   tl_trace.active = true;
   tl_trace.line[0] = 0;
@@ -482,9 +498,22 @@ void call_trace_end() {
   const auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
     return std::chrono::duration<double, std::milli>(b - a).count();
   };
-  if (tl_trace.line[0])
-    fprintf(stderr, "%s, entry %.4f ms, exit %.4f ms, call %.4f ms\n", tl_trace.line, ms(tl_trace.t_call0, tl_trace.t_run0),
-            ms(tl_trace.t_run1, t), ms(tl_trace.t_call0, t));
+  if (tl_trace.line[0]) {
+    char buf[400];
+    snprintf(buf, sizeof(buf), "%s, entry %.4f ms, exit %.4f ms, call %.4f ms", tl_trace.line, ms(tl_trace.t_call0, tl_trace.t_run0),
+             ms(tl_trace.t_run1, t), ms(tl_trace.t_call0, t));
+    if (call_trace_buffered()) {
+      std::lock_guard<std::mutex> lk(g_trace_mu);
+      if (!g_trace_lines) {
+        g_trace_lines = new std::vector<std::string>();
+        g_trace_lines->reserve(1 << 16);
+        atexit(print_trace_lines);
+      }
+      g_trace_lines->emplace_back(buf);
+    } else {
+      fprintf(stderr, "%s\n", buf);
+    }
+  }
   tl_trace.active = false;
   tl_trace.line[0] = 0;
 }

@@ -415,6 +415,10 @@ int run_host(PlanExt *e, char **ptrs, int nstripes, long long C, const std::vect
     const int r2 = unpack(stg->slot[(which + i) % kSlots]);
     if (!rc) rc = r2;
   }
+  if (rc == 0 && inplace.held()) {  // the in-place stall guard (ec_engine.h)
+    const size_t moved = static_cast<size_t>(nstripes) * (in_ids.size() + out_ids.size()) * static_cast<size_t>(C);
+    note_inplace_drain(moved, ms(t_loop0, now()));
+  }
   if (trace && rc == 0) {  // every slot drained: no transfer still reads or writes the pins
     const auto t_rel0 = now();
     inplace.release();  // (the destructor would, after this print)

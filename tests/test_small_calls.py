@@ -180,6 +180,22 @@ def test_fn_pointer_stress_bit_exact(cuda, chunk, threads, method, op, pinned, e
     assert rec["verified"] > 0 and rec["mismatches"] == 0, rec
 
 
+@pytest.mark.skipif(not (os.path.exists(BENCH) and os.path.exists(REF)), reason="build/fnptr_bench or oracle/_ref not built")
+def test_inplace_stall_guard_under_mmap_churn(cuda):
+    """Per-stripe 1 MiB decodes at two threads whose buffers are each a fresh mmap, munmapped right
+    after the call (FNPTR_FREE_AFTER=2): DMA from pages pinned in place stalls ~25 ms a call there
+    (profiles/r06_v2_free_after_churn.jsonl).  The stall guard (ec_engine.h) sees the stalls,
+    suspends in-place pinning and the calls pack: every call bit-exact, and the median call back
+    under a few milliseconds."""
+    env = dict(os.environ, FNPTR_VERIFY="1", FNPTR_REF=REF, FNPTR_FREE_AFTER="2")
+    out = subprocess.run([BENCH, str(1 << 20), "2", "3", "cauchy_good", "decode"], env=env, capture_output=True, text=True,
+                         timeout=100)
+    assert out.returncode == 0, (out.returncode, out.stdout[-500:], out.stderr[-500:])
+    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    assert rec["verified"] > 100 and rec["mismatches"] == 0, rec
+    assert rec["per_call_us_p50"] < 3000, (rec, out.stderr[-500:])
+
+
 STRESS = os.path.join(ROOT, "tools", "reg_stress.py")
 
 
