@@ -1243,7 +1243,8 @@ hipError_t launch(hipFunction_t fn, int R, int K, const ShardRef *in, const Shar
   const uint64_t ntiles = static_cast<uint64_t>((size + tile - 1) / tile) * static_cast<uint64_t>(nstripes);
   if (ntiles == 0) return hipSuccess;
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
-  return hipModuleLaunchKernel(fn, static_cast<unsigned>(ntiles), 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+  return hipModuleLaunchKernel(fn, static_cast<unsigned>(ntiles), 1, 1, 256, 1, 1,
+                               static_cast<unsigned>(lsec::occupancy_lds_bytes(size)), st, nullptr, cfg);
 }
 
 hipError_t launch_pkt(hipFunction_t fn, int R, int K, const ShardRef *in, const ShardRef *out, int nstripes, int64_t size,
@@ -1263,7 +1264,8 @@ hipError_t launch_pkt(hipFunction_t fn, int R, int K, const ShardRef *in, const 
   const uint64_t ntiles = static_cast<uint64_t>((cols + tile - 1) / tile) * static_cast<uint64_t>(nstripes) * S;
   if (ntiles == 0) return hipSuccess;
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
-  return hipModuleLaunchKernel(fn, static_cast<unsigned>(ntiles), 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+  return hipModuleLaunchKernel(fn, static_cast<unsigned>(ntiles), 1, 1, 256, 1, 1,
+                               static_cast<unsigned>(lsec::occupancy_lds_bytes(size)), st, nullptr, cfg);
 }
 
 void pkt_shape(int R, int w, int packet, int *D, int *S) {

@@ -40,6 +40,24 @@ hipError_t launch_kernel(void (*k)(KArgs...), dim3 grid, dim3 block, hipStream_t
   return launch_packed(reinterpret_cast<const void *>(k), grid, block, st, t, std::index_sequence_for<KArgs...>{});
 }
 
+// Occupancy cap of the streaming launches (launch_tiled's kernels and the compiled networks), as
+// unused dynamic LDS per workgroup: with it at most n workgroups share a CU's 160 KiB.  0 (the
+// default, or n = 0): no cap.  n from LSEC_WGS_CAP for launches whose shards are at least
+// LSEC_WGS_CAP_MIN_KB apart (A/B runs of the C = 8 MiB encode dip).
+size_t occupancy_lds_bytes(int64_t shard_bytes);
+template <typename T, size_t... I>
+hipError_t launch_packed_shm(const void *k, dim3 grid, dim3 block, size_t shm, hipStream_t st, T &args,
+                             std::index_sequence<I...>) {
+  void *ptrs[] = {static_cast<void *>(&std::get<I>(args))..., nullptr};
+  return hipLaunchKernel(k, grid, block, ptrs, shm, st);
+}
+template <typename... KArgs, typename... Args>
+hipError_t launch_kernel_shm(void (*k)(KArgs...), dim3 grid, dim3 block, size_t shm, hipStream_t st, const Args &...args) {
+  static_assert(sizeof...(KArgs) == sizeof...(Args), "argument count");
+  std::tuple<std::decay_t<KArgs>...> t(static_cast<std::decay_t<KArgs>>(args)...);
+  return launch_packed_shm(reinterpret_cast<const void *>(k), grid, block, shm, st, t, std::index_sequence_for<KArgs...>{});
+}
+
 constexpr int kMaxK = 64;   // input shards per launch (wider stripes: several launches, the later ones with
                             // ApplyArgs::accumulate, over images in the grouped layout below)
 constexpr int kMaxR = 16;   // output shards per launch

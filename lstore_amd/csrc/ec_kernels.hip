@@ -181,6 +181,21 @@ void tile_queue_release(hipStream_t st, unsigned *slot) {
   ss.busy.store(0, std::memory_order_release);
 }
 
+size_t occupancy_lds_bytes(int64_t shard_bytes) {
+  static const int cap = [] {
+    const char *e = getenv("LSEC_WGS_CAP");
+    return e ? std::max(0, atoi(e)) : 0;
+  }();
+  static const int64_t min_bytes = [] {
+    const char *e = getenv("LSEC_WGS_CAP_MIN_KB");
+    return e ? static_cast<int64_t>(atoll(e)) << 10 : 0;
+  }();
+  if (cap <= 0 || shard_bytes < min_bytes) return 0;
+  // 160 KiB of LDS per CU; 2 KiB left for the kernels' own static LDS
+  const size_t per = (160u << 10) / static_cast<size_t>(cap);
+  return per > (2u << 10) ? (per - (2u << 10)) & ~static_cast<size_t>(255) : 0;
+}
+
 int persistent_grid(const void *kernel, int grid, hipStream_t st) {
   const int dev = stream_device(st);
   if (dev < 0 || dev >= kQueueDevs || g_cus[dev] <= 0) return 0;
@@ -203,6 +218,11 @@ int persistent_grid(const void *kernel, int grid, hipStream_t st) {
     return e ? atoi(e) : 0;
   }();
   if (force > 0) n = force;
+  static const int cap = [] {  // LSEC_WGS_CAP (occupancy_lds_bytes): no more persistent blocks than fit
+    const char *e = getenv("LSEC_WGS_CAP");
+    return e ? std::max(0, atoi(e)) : 0;
+  }();
+  if (cap > 0 && n > cap) n = cap;
   if (n <= 0) return 0;
   // a multiple of 8: every XCD the same number of workgroups (blocks are dealt round-robin)
   const int full = n * g_cus[dev];

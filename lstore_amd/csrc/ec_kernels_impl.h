@@ -176,7 +176,7 @@ hipError_t launch_tiled(Kern *k, int grid, hipStream_t st, ApplyArgs a) {
       grid = static_cast<int>(8 * a.tiles_pre) + pg;
     }
   }
-  const hipError_t e = launch_kernel(k, dim3(grid), dim3(kBlock), st, a);
+  const hipError_t e = launch_kernel_shm(k, dim3(grid), dim3(kBlock), occupancy_lds_bytes(a.size), st, a);
   tile_queue_release(st, slot);
   return e;
 }

@@ -31,6 +31,9 @@ CONFIGS = {
     "cg104m": (L.CAUCHY_GOOD, 10, 4, 512 << 10),
     "cg104l": (L.CAUCHY_GOOD, 10, 4, 2 << 20),
     "cg164c8": (L.CAUCHY_GOOD, 16, 4, 8 << 20),
+    "cg164c1": (L.CAUCHY_GOOD, 16, 4, 1 << 20),
+    "cg206c1": (L.CAUCHY_GOOD, 20, 6, 1 << 20),
+    "cg206c8": (L.CAUCHY_GOOD, 20, 6, 8 << 20),
     "cg124c4": (L.CAUCHY_GOOD, 12, 4, 4 << 20),
     "cg124c8": (L.CAUCHY_GOOD, 12, 4, 8 << 20),
     "rs164": (L.REED_SOL_VAN, 16, 4, 1 << 20),
