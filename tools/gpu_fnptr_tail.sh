@@ -10,7 +10,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 export FNPTR_REF=oracle/_ref/libjerasure_ref.so
 o=gpurun_out/fnptr_tail_${tag}
-LSEC_TRACE=2 FNPTR_LAT_OUT=$o.lat.txt timeout -k 10 90 build/fnptr_bench 1048576 1 5 cauchy_good decode \
+env -u FNPTR_REF LSEC_TRACE=2 FNPTR_LAT_OUT=$o.lat.txt timeout -k 10 90 build/fnptr_bench 1048576 1 5 cauchy_good decode \
   > $o.traced.jsonl 2> $o.trace.txt || { echo "traced run failed"; tail -5 $o.trace.txt; exit 1; }
 python tools/tail_join.py $o.trace.txt $o.lat.txt > $o.join.jsonl || { echo "join failed"; exit 1; }
 cat $o.join.jsonl
