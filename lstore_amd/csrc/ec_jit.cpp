@@ -137,6 +137,16 @@ bool wants_xornet(int R, int K) {
 // 8-15 shared-pair cap, 16 unfenced loads, 17-18 inputs ahead, 21 serial XOR folds (gfw_source);
 // 19 turns the wave-pair split of 4-row w = 32 networks off, 20-23 shape it
 // (gfw_rowsplit_source; profiles/r04_v7_gfw_w32_ab.md, r04_v9_gfw_w32_split.txt).
+// The first tile of a block (one tile per block, XCD x taking a contiguous eighth of the tiles in
+// dispatch order), as the generated kernels compute it.  Args::phase > 0 (the XCD tile phase,
+// lsec::tile_phase_on, ec_kernels.h): XCD x starts its eighth x * phase tiles further on and wraps
+// around inside it, so the eight XCDs stream from different column offsets of their stripes.
+std::string tile_start() {
+  return "  const unsigned sz_ = per + (xcd < rem ? 1u : 0u);\n"
+         "  const unsigned ph_ = (nb == nt && sz_) ? (xcd * a.phase) % sz_ : 0u;\n"
+         "  const unsigned t0 = xcd * per + (xcd < rem ? xcd : rem) + (ph_ ? ((blockIdx.x >> 3) + ph_) % sz_ : (blockIdx.x >> 3));\n";
+}
+
 int jit_variant() {
   static const int v = [] {
     const char *s = getenv("LSEC_JIT_VARIANT");
@@ -237,7 +247,7 @@ std::string xornet_source(const uint8_t *mat, int R, int K) {
        "typedef u32 u32x4 __attribute__((ext_vector_type(4)));\n"
        "typedef u32 u32x2 __attribute__((ext_vector_type(2)));\n"
        "struct Ref { unsigned long long base; long long stride; };\n"
-    << "struct Args { long long size; int nstripes; int pad; Ref in[" << K << "]; Ref out[" << R << "]; };\n"
+    << "struct Args { long long size; int nstripes; int pad; Ref in[" << K << "]; Ref out[" << R << "]; unsigned phase; };\n"
     << "#define X3(a,b,c) __builtin_amdgcn_bitop3_b32((a),(b),(c),0x96)\n";
   if (!(var & 2)) {
     // x * (4 packed GF(2^8) elements), polynomial 0x11D: shift, and 0x1D times the bit-7 flags
@@ -290,7 +300,7 @@ std::string xornet_source(const uint8_t *mat, int R, int K) {
     << "  const unsigned tps = (unsigned)((C + " << tile - 1 << ") / " << tile << ");\n"
     << "  const unsigned nt = tps * (unsigned)a.nstripes;\n"
        "  const unsigned nb = gridDim.x, per = nb >> 3, rem = nb & 7, xcd = blockIdx.x & 7;\n"
-       "  const unsigned t0 = xcd * per + (xcd < rem ? xcd : rem) + (blockIdx.x >> 3);\n"
+    << tile_start() <<
        "  for (unsigned t = t0; t < nt; t += nb) {\n"
        "    const unsigned s = t / tps;\n"
     << "    const long long o0 = (long long)(t - s * tps) * " << tile << " + threadIdx.x * " << 4 * D << ";\n";
@@ -398,7 +408,7 @@ void gfw_prelude(std::ostringstream &s, int R, int K, int W, int stride) {
        "typedef u32 u32x4 __attribute__((ext_vector_type(4)));\n"
        "typedef u32 u32x2 __attribute__((ext_vector_type(2)));\n"
        "struct Ref { unsigned long long base; long long stride; };\n"
-    << "struct Args { long long size; int nstripes; int pad; Ref in[" << K << "]; Ref out[" << R << "]; };\n"
+    << "struct Args { long long size; int nstripes; int pad; Ref in[" << K << "]; Ref out[" << R << "]; unsigned phase; };\n"
     << "#define W " << W << "\n"
     << "#define PIECE " << stride << "\n"
        "#define X3(a,b,c) __builtin_amdgcn_bitop3_b32((a),(b),(c),0x96)\n"
@@ -552,7 +562,7 @@ std::string gfw_rowsplit_source(const uint32_t *mat, int R, int K, int W) {
     << "  const unsigned tps = (unsigned)(C / " << tile << ");\n"
     << "  const unsigned nt = tps * (unsigned)a.nstripes;\n"
        "  const unsigned nb = gridDim.x, per = nb >> 3, rem = nb & 7, xcd = blockIdx.x & 7;\n"
-       "  const unsigned t0 = xcd * per + (xcd < rem ? xcd : rem) + (blockIdx.x >> 3);\n"
+    << tile_start() <<
        "  for (unsigned t = t0; t < nt; t += nb) {\n"
        "    const unsigned s = t / tps;\n"
     << "    const long long base = (long long)(t - s * tps) * " << tile << " + (pair * 64 + lane) * 16;\n";
@@ -682,7 +692,7 @@ std::string pktnet_source(const uint32_t *masks, int R, int K, int W, int D, int
        "typedef u32 u32x4 __attribute__((ext_vector_type(4)));\n"
        "typedef u32 u32x2 __attribute__((ext_vector_type(2)));\n"
        "struct Ref { unsigned long long base; long long stride; };\n"
-    << "struct Args { long long size; int nstripes; int packet; Ref in[" << K << "]; Ref out[" << R << "]; };\n"
+    << "struct Args { long long size; int nstripes; int packet; Ref in[" << K << "]; Ref out[" << R << "]; unsigned phase; };\n"
     << "typedef " << vt << " V;\n"
        "#define X3(a,b,c) __builtin_amdgcn_bitop3_b32((a),(b),(c),0x96)\n"
        "#define G(a) ((const __attribute__((address_space(1))) V *)(a))\n"
@@ -703,7 +713,7 @@ std::string pktnet_source(const uint32_t *masks, int R, int K, int W, int D, int
     << "  const unsigned tps = (cols + " << tile - 1 << ") / " << tile << ";\n"
     << "  const unsigned nt = tps * (unsigned)a.nstripes * " << S << "u;\n"
        "  const unsigned nb = gridDim.x, per = nb >> 3, rem = nb & 7, xcd = blockIdx.x & 7;\n"
-       "  const unsigned t0 = xcd * per + (xcd < rem ? xcd : rem) + (blockIdx.x >> 3);\n"
+    << tile_start() <<
        "  for (unsigned t = t0; t < nt; t += nb) {\n"
     << "    const unsigned g = t % " << S << "u, ct = t / " << S << "u;\n"
        "    const unsigned s = ct / tps;\n"
@@ -809,7 +819,7 @@ std::string gfw_source(const uint32_t *mat, int R, int K, int W) {
     << "  const unsigned tps = (unsigned)(C / " << tile << ");\n"
     << "  const unsigned nt = tps * (unsigned)a.nstripes;\n"
        "  const unsigned nb = gridDim.x, per = nb >> 3, rem = nb & 7, xcd = blockIdx.x & 7;\n"
-       "  const unsigned t0 = xcd * per + (xcd < rem ? xcd : rem) + (blockIdx.x >> 3);\n"
+    << tile_start() <<
        "  for (unsigned t = t0; t < nt; t += nb) {\n"
        "    const unsigned s = t / tps;\n"
     << "    const long long base = (long long)(t - s * tps) * " << tile << " + threadIdx.x * 16;\n";
@@ -1232,14 +1242,18 @@ hipFunction_t ready(const void *image, int R, int K) {
 hipError_t launch(hipFunction_t fn, int R, int K, const ShardRef *in, const ShardRef *out, int nstripes, int64_t size,
                   hipStream_t st, int w) {
   // struct Args { long long size; int nstripes; int pad; Ref in[K]; Ref out[R]; }
-  std::vector<uint8_t> args(16 + sizeof(ShardRef) * (K + R));
+  // struct Args { ...; Ref out[R]; unsigned phase; } (8-byte aligned size)
+  std::vector<uint8_t> args(16 + sizeof(ShardRef) * (K + R) + 8, 0);
   std::memcpy(args.data(), &size, 8);
   std::memcpy(args.data() + 8, &nstripes, 4);
   std::memcpy(args.data() + 16, in, sizeof(ShardRef) * K);
   std::memcpy(args.data() + 16 + sizeof(ShardRef) * K, out, sizeof(ShardRef) * R);
+  const int64_t tile = w == 8 ? xornet_tile(K, R) : gfw_tile(w, R);  // as xornet_source / gfw_source
+  const uint64_t tps = w == 8 ? static_cast<uint64_t>((size + tile - 1) / tile) : static_cast<uint64_t>(size / tile);
+  const uint32_t phase = lsec::tile_phase_on() ? static_cast<uint32_t>(tps / 8) : 0;
+  std::memcpy(args.data() + 16 + sizeof(ShardRef) * (K + R), &phase, 4);
   size_t bytes = args.size();
   void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes, HIP_LAUNCH_PARAM_END};
-  const int64_t tile = w == 8 ? xornet_tile(K, R) : gfw_tile(w, R);  // as xornet_source / gfw_source
   const uint64_t ntiles = static_cast<uint64_t>((size + tile - 1) / tile) * static_cast<uint64_t>(nstripes);
   if (ntiles == 0) return hipSuccess;
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
@@ -1250,18 +1264,21 @@ hipError_t launch(hipFunction_t fn, int R, int K, const ShardRef *in, const Shar
 hipError_t launch_pkt(hipFunction_t fn, int R, int K, const ShardRef *in, const ShardRef *out, int nstripes, int64_t size,
                       int packet, int w, hipStream_t st) {
   // struct Args { long long size; int nstripes; int packet; Ref in[K]; Ref out[R]; }
-  std::vector<uint8_t> args(16 + sizeof(ShardRef) * (K + R));
+  std::vector<uint8_t> args(16 + sizeof(ShardRef) * (K + R) + 8, 0);  // (+ unsigned phase, 8-byte aligned)
   std::memcpy(args.data(), &size, 8);
   std::memcpy(args.data() + 8, &nstripes, 4);
   std::memcpy(args.data() + 12, &packet, 4);
   std::memcpy(args.data() + 16, in, sizeof(ShardRef) * K);
   std::memcpy(args.data() + 16 + sizeof(ShardRef) * K, out, sizeof(ShardRef) * R);
-  size_t bytes = args.size();
-  void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes, HIP_LAUNCH_PARAM_END};
   int D = 0, S = 1;
   pkt_shape(R, w, packet, &D, &S);  // as bind_pkt
   const int64_t tile = 256 * 4 * D, cols = size / w;  // column bytes of a stripe: nsuper * packet
-  const uint64_t ntiles = static_cast<uint64_t>((cols + tile - 1) / tile) * static_cast<uint64_t>(nstripes) * S;
+  const uint64_t tps = static_cast<uint64_t>((cols + tile - 1) / tile) * S;  // tiles per stripe
+  const uint32_t phase = lsec::tile_phase_on() ? static_cast<uint32_t>(tps / 8) : 0;
+  std::memcpy(args.data() + 16 + sizeof(ShardRef) * (K + R), &phase, 4);
+  size_t bytes = args.size();
+  void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes, HIP_LAUNCH_PARAM_END};
+  const uint64_t ntiles = tps * static_cast<uint64_t>(nstripes);
   if (ntiles == 0) return hipSuccess;
   if (ntiles >= (1ull << 31)) return hipErrorInvalidValue;
   return hipModuleLaunchKernel(fn, static_cast<unsigned>(ntiles), 1, 1, 256, 1, 1,

@@ -181,6 +181,23 @@ void tile_queue_release(hipStream_t st, unsigned *slot) {
   ss.busy.store(0, std::memory_order_release);
 }
 
+namespace {
+std::atomic<int> g_tile_phase{-1};  // -1: not read from LSEC_TILE_PHASE yet
+}  // namespace
+
+bool tile_phase_on() {
+  int v = g_tile_phase.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char *e = getenv("LSEC_TILE_PHASE");
+    v = e && *e == '1' ? 1 : 0;
+    int expect = -1;
+    if (!g_tile_phase.compare_exchange_strong(expect, v)) v = expect;
+  }
+  return v == 1;
+}
+
+void set_tile_phase(int on) { g_tile_phase.store(on ? 1 : 0, std::memory_order_relaxed); }
+
 size_t occupancy_lds_bytes(int64_t shard_bytes) {
   static const int cap = [] {
     const char *e = getenv("LSEC_WGS_CAP");
@@ -492,7 +509,7 @@ __global__ __launch_bounds__(kBlock) void k_hbm_mix(ApplyArgs a) {
         }
       }
     }
-  });
+  }, a.tile_phase);
 }
 
 // Decode-shape probe (measurement only; shares no code with the coding kernels or their tile

@@ -111,10 +111,18 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
 //   trip hides behind the grab's tiles; it posts the grab in one of two LDS words (never one a wave
 //   has yet to read: that wave has not passed the barrier after its read), and readfirstlane keeps
 //   the loop uniform.  One call site of body for every form: the kernels' code is not repeated.
+//   phase > 0 (ApplyArgs::tile_phase): XCD / eighth x visits its tiles starting x * phase tiles in,
+//   wrapping around inside its own range (a bijection; the static form only when the grid is the
+//   tile count).
 template <int G = 1, typename Body>
-__device__ __forceinline__ void for_tiles(uint32_t ntiles, unsigned *q, uint32_t pre, Body &&body) {
+__device__ __forceinline__ void for_tiles(uint32_t ntiles, unsigned *q, uint32_t pre, Body &&body, uint32_t phase = 0) {
   __shared__ uint32_t next[2];
   const uint32_t per = (ntiles + 7) >> 3, xcd = blockIdx.x & 7;
+  // the phase's map of a queue-form tile index: eighth e = t / per, rotated inside its own range
+  const auto rot = [&](uint32_t t) -> uint32_t {
+    const uint32_t e = t / per, base = e * per, size = min(per, ntiles - base);
+    return base + ((t - base) + (e * phase) % size) % size;
+  };
   const bool sharing = q != nullptr && blockIdx.x >= 8 * pre;  // block-uniform
   const uint32_t rest = per - pre, grabs = (rest + G - 1) / G;  // each eighth's shared tiles, grabs
   uint32_t k = 0, pend = 0, it = 0;  // thread 0: eighths done, the counter value in flight
@@ -129,6 +137,11 @@ __device__ __forceinline__ void for_tiles(uint32_t ntiles, unsigned *q, uint32_t
   uint32_t t, end, step = 1;
   if (q == nullptr) {
     t = xcd_remap(blockIdx.x, gridDim.x);
+    if (phase && gridDim.x == ntiles) {  // one tile per block: rotate inside this XCD's contiguous run
+      const uint32_t nb = gridDim.x, p8 = nb >> 3, rem = nb & 7;
+      const uint32_t size = p8 + (xcd < rem ? 1u : 0u), start = xcd * p8 + min(xcd, rem);
+      t = start + ((blockIdx.x >> 3) + (xcd * phase) % size) % size;
+    }
     end = ntiles;
     step = gridDim.x;
   } else if (!sharing) {  // the static prefix: one tile
@@ -151,7 +164,7 @@ __device__ __forceinline__ void for_tiles(uint32_t ntiles, unsigned *q, uint32_t
       end = min(min(ntiles, (t / per + 1) * per), t + G);  // a grab stays inside its eighth
       if (threadIdx.x == 0) pend = atomicAdd(q + kTileQueueLine * ((xcd + k) & 7), 1u);  // the next grab
     }
-    body(t);
+    body(q != nullptr && phase ? rot(t) : t);
     t += step;
   }
   // the launch's last sharing block leaves the slot zeroed for its next taker
@@ -164,6 +177,8 @@ __device__ __forceinline__ void for_tiles(uint32_t ntiles, unsigned *q, uint32_t
 template <typename Kern>
 hipError_t launch_tiled(Kern *k, int grid, hipStream_t st, ApplyArgs a) {
   a.stamps = launch_stamps(&a.nstamps);
+  // `grid` is the tile count here: tiles per stripe = grid / nstripes
+  a.tile_phase = tile_phase_on() && a.nstripes > 0 && grid % a.nstripes == 0 ? static_cast<uint32_t>(grid / a.nstripes / 8) : 0;
   unsigned *slot = tile_queue_slot(st, static_cast<uint64_t>(grid));
   a.tiles = nullptr;
   a.tiles_pre = 0;
@@ -511,7 +526,7 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
       bw_magic_out<R, IT, VW>(ml, K, acc);
       ml_commit(ml, a.magic_acc, s, K + R, static_cast<uint64_t>(a.size), static_cast<uint64_t>(off0), kStep, red);
     }
-  });
+  }, a.tile_phase);
 }
 
 // The XOR-row flag (CoefCell::pad bit 0 of the launch's first cell) picks one of two whole
@@ -611,7 +626,7 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
       }
     }
     if constexpr (MG) ml_commit(ml, a.magic_acc, s, K + R, static_cast<uint64_t>(a.size), static_cast<uint64_t>(off), P, red);
-  });
+  }, a.tile_phase);
 }
 
 // ------------------------------------------------------------------ generic bitmatrix

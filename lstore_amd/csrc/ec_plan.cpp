@@ -1105,6 +1105,10 @@ void lsec_test_set_stamps(void *dev_buf, unsigned n) {
   lsec::set_launch_stamps(static_cast<unsigned long long *>(dev_buf), n);
 }
 
+// Test hook, not in include/: the XCD tile phase on (1) or off (0) for the following launches
+// (lsec::tile_phase_on; LSEC_TILE_PHASE sets the start value), for A/B runs in one allocation.
+void lsec_test_set_tile_phase(int on) { lsec::set_tile_phase(on); }
+
 
 // Self-test of the bitmatrix decode planner (test hook, not in include/; no GPU): for the
 // liberation-family plan (method, k, w) with m = 2, make_bit_decode's masks must equal those of

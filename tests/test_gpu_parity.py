@@ -1331,3 +1331,41 @@ def test_staging_pool_keeps_at_most_two_large_device_halves(cuda):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, "-c", POOL_SCRIPT, root], capture_output=True, text=True, timeout=110)
     assert out.returncode == 0 and out.stdout.strip().endswith("ok"), (out.stdout[-800:], out.stderr[-1500:])
+
+
+@pytest.mark.parametrize("method,k,m,C,n,w", [
+    (L.REED_SOL_VAN, 6, 3, 1 << 20, 64, 8),        # K1, tile queue (static 7/8 + shared tail)
+    (L.REED_SOL_VAN, 6, 3, 65536 + 8, 9, 8),       # K1, static eighths, ragged last tile
+    (L.CAUCHY_GOOD, 10, 4, 4 << 20, 12, 8),        # compiled packet network
+    (L.REED_SOL_VAN, 20, 6, 256 << 10, 40, 8),     # compiled XOR network
+    (L.REED_SOL_VAN, 10, 4, 1 << 20, 10, 16),      # compiled w = 16 network
+])
+def test_xcd_tile_phase_is_bit_identical(cuda, method, k, m, C, n, w):
+    """The XCD tile phase (lsec_test_set_tile_phase; ApplyArgs::tile_phase, the networks' Args::phase)
+    only changes which tile a workgroup takes: encode and single-erasure decode write the same bytes
+    with it on and off, in the bytewise kernel's queue and static forms and in the compiled networks."""
+    import torch
+
+    lib = L.lib()
+    with L.Plan.for_chunk(method, k, m, C, w) as p:
+        p.prepare_encode()
+        p.prepare_decode([1])
+        g = torch.Generator(device=cuda).manual_seed(C + k)
+        d = torch.randint(0, 256, (n, k, C), dtype=torch.uint8, device=cuda, generator=g)
+        outs = []
+        try:
+            for phase in (0, 1, 0):
+                lib.lsec_test_set_tile_phase(phase)
+                par = torch.zeros((n, m, C), dtype=torch.uint8, device=cuda)
+                p.encode_dev(d, par)
+                rb = torch.zeros((n, 1, C), dtype=torch.uint8, device=cuda)
+                p.decode_dev(d, par, [1], out=rb)
+                torch.cuda.synchronize()
+                outs.append((par, rb))
+        finally:
+            lib.lsec_test_set_tile_phase(0)
+        for par, rb in outs[1:]:
+            assert torch.equal(par, outs[0][0])
+            assert torch.equal(rb[:, 0], d[:, 1])
+        hp = outs[0][0][0].cpu().numpy()
+        assert np.array_equal(hp, O.encode(method, d[0].cpu().numpy(), m, p.packet_size, w=w))

@@ -127,7 +127,9 @@ def main():
                 tmix.append(e0.elapsed_time(e1) / a.reps)
                 plan.encode_dev(data, par)  # restore the parity the variants are checked against
             for v in variants:
-                E.set_kernel_variant(*v)
+                E.set_kernel_variant(v[0], v[1])
+                if len(v) > 2:  # a third field: the XCD tile phase (lsec_test_set_tile_phase)
+                    E.lib().lsec_test_set_tile_phase(v[2])
                 e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
                 plan.encode_dev(data, par)
                 e0.record(stream)
@@ -149,7 +151,7 @@ def main():
             td = sorted(res[v][1])[len(res[v][1]) // 2]
             eb = (k + m) * C * N
             db = (k + len(lost)) * C * N
-            print(f"{name:6s} N={N:5d} variant={v} jit={int(plan.jit()) if v == (0, 0) else 0}  encode {te:8.3f} ms {eb / te / 1e6:7.1f} GB/s "
+            print(f"{name:6s} N={N:5d} variant={v} jit={int(plan.jit()) if v[:2] == (0, 0) else 0}  encode {te:8.3f} ms {eb / te / 1e6:7.1f} GB/s "
                   f"({eb / te / 8e9:5.1%})   decode {td:8.3f} ms {db / td / 1e6:7.1f} GB/s ({db / td / 8e9:5.1%})",
                   flush=True)
         if tmix:
@@ -158,6 +160,7 @@ def main():
             print(f"{name:6s} N={N:5d} mix probe (XOR of k to m, no GF)  {tm:8.3f} ms {eb / tm / 1e6:7.1f} GB/s ({eb / tm / 8e9:5.1%})",
                   flush=True)
         E.set_kernel_variant(0, 0)
+        E.lib().lsec_test_set_tile_phase(0)
         if a.magic:
             mg = torch.zeros((N, 4), dtype=torch.uint8, device=dev)
             tm = []
