@@ -32,6 +32,10 @@ CONFIGS = {
     "cg104l": (L.CAUCHY_GOOD, 10, 4, 2 << 20),
     "cg164c8": (L.CAUCHY_GOOD, 16, 4, 8 << 20),
     "cg164c1": (L.CAUCHY_GOOD, 16, 4, 1 << 20),
+    "rs84c4": (L.REED_SOL_VAN, 8, 4, 4 << 20),
+    "rs83c8": (L.REED_SOL_VAN, 8, 3, 8 << 20),
+    "rs164c8": (L.REED_SOL_VAN, 16, 4, 8 << 20),
+    "rs63c8": (L.REED_SOL_VAN, 6, 3, 8 << 20),
     "cg206c1": (L.CAUCHY_GOOD, 20, 6, 1 << 20),
     "cg206c8": (L.CAUCHY_GOOD, 20, 6, 8 << 20),
     "cg124c4": (L.CAUCHY_GOOD, 12, 4, 4 << 20),
