@@ -198,6 +198,23 @@ bool tile_phase_on() {
 
 void set_tile_phase(int on) { g_tile_phase.store(on ? 1 : 0, std::memory_order_relaxed); }
 
+namespace {
+std::atomic<int> g_mem_mode{-1};  // -1: not read from LSEC_MEM_MODE yet
+}  // namespace
+
+int mem_mode() {
+  int v = g_mem_mode.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char *e = getenv("LSEC_MEM_MODE");
+    v = e ? (atoi(e) & 3) : 0;
+    int expect = -1;
+    if (!g_mem_mode.compare_exchange_strong(expect, v)) v = expect;
+  }
+  return v;
+}
+
+void set_mem_mode(int mode) { g_mem_mode.store(mode & 3, std::memory_order_relaxed); }
+
 size_t occupancy_lds_bytes(int64_t shard_bytes) {
   static const int cap = [] {
     const char *e = getenv("LSEC_WGS_CAP");

@@ -1109,6 +1109,10 @@ void lsec_test_set_stamps(void *dev_buf, unsigned n) {
 // (lsec::tile_phase_on; LSEC_TILE_PHASE sets the start value), for A/B runs in one allocation.
 void lsec_test_set_tile_phase(int on) { lsec::set_tile_phase(on); }
 
+// Test hook, not in include/: the bytewise / bit-sliced kernels' memory-instruction mode (bit 0 plain
+// stores, bit 1 plain loads; 0 non-temporal, the default) for the following launches (A/B runs).
+void lsec_test_set_mem_mode(int mode) { lsec::set_mem_mode(mode); }
+
 
 // Self-test of the bitmatrix decode planner (test hook, not in include/; no GPU): for the
 // liberation-family plan (method, k, w) with m = 2, make_bit_decode's masks must equal those of
