@@ -139,8 +139,8 @@ bool wants_xornet(int R, int K) {
 // (gfw_rowsplit_source; profiles/r04_v7_gfw_w32_ab.md, r04_v9_gfw_w32_split.txt).
 // The first tile of a block (one tile per block, XCD x taking a contiguous eighth of the tiles in
 // dispatch order), as the generated kernels compute it.  Args::phase > 0 (the XCD tile phase,
-// lsec::tile_phase_on, ec_kernels.h): XCD x starts its eighth x * phase tiles further on and wraps
-// around inside it, so the eight XCDs stream from different column offsets of their stripes.
+// lsec::tile_phase_net_on, ec_kernels.h; off by default for the networks): XCD x starts its eighth
+// x * phase tiles further on and wraps around inside it.
 std::string tile_start() {
   return "  const unsigned sz_ = per + (xcd < rem ? 1u : 0u);\n"
          "  const unsigned ph_ = (nb == nt && sz_) ? (xcd * a.phase) % sz_ : 0u;\n"
@@ -1250,7 +1250,7 @@ hipError_t launch(hipFunction_t fn, int R, int K, const ShardRef *in, const Shar
   std::memcpy(args.data() + 16 + sizeof(ShardRef) * K, out, sizeof(ShardRef) * R);
   const int64_t tile = w == 8 ? xornet_tile(K, R) : gfw_tile(w, R);  // as xornet_source / gfw_source
   const uint64_t tps = w == 8 ? static_cast<uint64_t>((size + tile - 1) / tile) : static_cast<uint64_t>(size / tile);
-  const uint32_t phase = lsec::tile_phase_on() ? static_cast<uint32_t>(tps / 8) : 0;
+  const uint32_t phase = lsec::tile_phase_net_on() ? static_cast<uint32_t>(tps / 8) : 0;
   std::memcpy(args.data() + 16 + sizeof(ShardRef) * (K + R), &phase, 4);
   size_t bytes = args.size();
   void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes, HIP_LAUNCH_PARAM_END};
@@ -1274,7 +1274,7 @@ hipError_t launch_pkt(hipFunction_t fn, int R, int K, const ShardRef *in, const 
   pkt_shape(R, w, packet, &D, &S);  // as bind_pkt
   const int64_t tile = 256 * 4 * D, cols = size / w;  // column bytes of a stripe: nsuper * packet
   const uint64_t tps = static_cast<uint64_t>((cols + tile - 1) / tile) * S;  // tiles per stripe
-  const uint32_t phase = lsec::tile_phase_on() ? static_cast<uint32_t>(tps / 8) : 0;
+  const uint32_t phase = lsec::tile_phase_net_on() ? static_cast<uint32_t>(tps / 8) : 0;
   std::memcpy(args.data() + 16 + sizeof(ShardRef) * (K + R), &phase, 4);
   size_t bytes = args.size();
   void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, args.data(), HIP_LAUNCH_PARAM_BUFFER_SIZE, &bytes, HIP_LAUNCH_PARAM_END};

@@ -110,7 +110,6 @@ struct ApplyArgs {
   unsigned long long *stamps;  // measurement only (lsec_test_set_stamps): each workgroup's end time, or null
   uint32_t nstamps;
   uint32_t tile_phase;    // XCD tile phase (tile_phase_on): XCD x starts its eighth x * tile_phase tiles on, 0 = off
-  uint32_t mem_mode;      // bit 0: plain stores, bit 1: plain loads (mem_mode(); A/B runs), 0 = non-temporal
   ShardRef in[kMaxK];
   ShardRef out[kMaxR];
 };
@@ -132,15 +131,13 @@ constexpr int kTileQueueRing = 4096;
 // launch small (fewer than kTileQueueMinTiles), or no slot available (the static eighths serve)
 constexpr uint64_t kTileQueueMinTiles = 16384;
 unsigned *tile_queue_slot(hipStream_t st, uint64_t ntiles);
-// XCD tile phase (LSEC_TILE_PHASE=1, A/B of the C = 8 MiB encode dip): every XCD's eighth of the tiles
-// starts 1/8 of a stripe later than the previous XCD's (wrapping around inside the eighth), so the
-// eight XCDs stream from different column offsets of their stripes at any moment
+// XCD tile phase: every XCD's eighth of the tiles starts 1/8 of a stripe later than the previous
+// XCD's (wrapping around inside the eighth), so the eight XCDs stream from different column offsets
+// of their stripes at any moment.  On for launch_tiled's kernels (tile_phase_on), off for the
+// compiled networks (tile_phase_net_on); LSEC_TILE_PHASE = bit 0 | bit 1 << 1 overrides (default 1)
 bool tile_phase_on();
-void set_tile_phase(int on);  // (lsec_test_set_tile_phase: A/B runs in one process)
-// memory-instruction mode of the bytewise / bit-sliced kernels (ApplyArgs::mem_mode; LSEC_MEM_MODE,
-// lsec_test_set_mem_mode): 0 non-temporal loads and stores (default)
-int mem_mode();
-void set_mem_mode(int mode);
+bool tile_phase_net_on();
+void set_tile_phase(int mode);  // (lsec_test_set_tile_phase: A/B runs in one process)
 // after the launch that took `slot` is queued on st: records the slot's event and frees it for a
 // later taker (who waits for that event first: a slot is never shared by two unfinished launches)
 void tile_queue_release(hipStream_t st, unsigned *slot);

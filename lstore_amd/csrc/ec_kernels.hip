@@ -182,38 +182,28 @@ void tile_queue_release(hipStream_t st, unsigned *slot) {
 }
 
 namespace {
-std::atomic<int> g_tile_phase{-1};  // -1: not read from LSEC_TILE_PHASE yet
-}  // namespace
+// bit 0: the tile loops of launch_tiled's kernels, bit 1: the compiled networks; -1: not read from
+// LSEC_TILE_PHASE yet (unset: 1, the measured default -- RS(8+4) at 4-8 MiB +1.1-1.7 %, every other
+// shape level, the networks level or -0.6 %: profiles/r06_v7_tile_phase_ab.txt,
+// r06_v10_tile_phase_mem_mode_ab.txt)
+std::atomic<int> g_tile_phase{-1};
 
-bool tile_phase_on() {
+int tile_phase_mode() {
   int v = g_tile_phase.load(std::memory_order_relaxed);
   if (v < 0) {
     const char *e = getenv("LSEC_TILE_PHASE");
-    v = e && *e == '1' ? 1 : 0;
+    v = e && *e ? (atoi(e) & 3) : 1;
     int expect = -1;
     if (!g_tile_phase.compare_exchange_strong(expect, v)) v = expect;
   }
-  return v == 1;
-}
-
-void set_tile_phase(int on) { g_tile_phase.store(on ? 1 : 0, std::memory_order_relaxed); }
-
-namespace {
-std::atomic<int> g_mem_mode{-1};  // -1: not read from LSEC_MEM_MODE yet
-}  // namespace
-
-int mem_mode() {
-  int v = g_mem_mode.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char *e = getenv("LSEC_MEM_MODE");
-    v = e ? (atoi(e) & 3) : 0;
-    int expect = -1;
-    if (!g_mem_mode.compare_exchange_strong(expect, v)) v = expect;
-  }
   return v;
 }
+}  // namespace
 
-void set_mem_mode(int mode) { g_mem_mode.store(mode & 3, std::memory_order_relaxed); }
+bool tile_phase_on() { return (tile_phase_mode() & 1) != 0; }
+bool tile_phase_net_on() { return (tile_phase_mode() & 2) != 0; }
+
+void set_tile_phase(int mode) { g_tile_phase.store(mode & 3, std::memory_order_relaxed); }
 
 size_t occupancy_lds_bytes(int64_t shard_bytes) {
   static const int cap = [] {

@@ -72,19 +72,6 @@ __device__ __forceinline__ void put_nt(uint64_t q, V v) {
   if constexpr (ACC) v ^= *gptr<V>(q);
   __builtin_nontemporal_store(v, gptr_w<V>(q));
 }
-// Memory-instruction mode of the bytewise and bit-sliced kernels (ApplyArgs::mem_mode, A/B runs,
-// lsec_test_set_mem_mode): bit 0 = plain (temporal) stores for the outputs, bit 1 = plain loads for
-// the inputs; 0 = non-temporal both ways, the default.  A wave-uniform branch.
-template <bool ACC, typename V>
-__device__ __forceinline__ void put_mode(uint64_t q, V v, uint32_t mode) {
-  if constexpr (ACC) v ^= *gptr<V>(q);
-  if (mode & 1u) *gptr_w<V>(q) = v;
-  else __builtin_nontemporal_store(v, gptr_w<V>(q));
-}
-template <typename V>
-__device__ __forceinline__ V get_mode(uint64_t p, uint32_t mode) {
-  return (mode & 2u) ? *gptr<V>(p) : __builtin_nontemporal_load(gptr<V>(p));
-}
 template <bool ACC, typename V>
 __device__ __forceinline__ void put(uint64_t q, V v) {
   if constexpr (ACC) v ^= *gptr<V>(q);
@@ -192,7 +179,6 @@ hipError_t launch_tiled(Kern *k, int grid, hipStream_t st, ApplyArgs a) {
   a.stamps = launch_stamps(&a.nstamps);
   // `grid` is the tile count here: tiles per stripe = grid / nstripes
   a.tile_phase = tile_phase_on() && a.nstripes > 0 && grid % a.nstripes == 0 ? static_cast<uint32_t>(grid / a.nstripes / 8) : 0;
-  a.mem_mode = static_cast<uint32_t>(mem_mode());
   unsigned *slot = tile_queue_slot(st, static_cast<uint64_t>(grid));
   a.tiles = nullptr;
   a.tiles_pre = 0;
@@ -455,7 +441,7 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
         for (int j = 0; j < KC; ++j) {
           const uint64_t p = a.in[j].base + s * a.in[j].stride + off0;
 #pragma unroll
-          for (int it = 0; it < IT; ++it) v[j][it] = get_mode<V>(p + it * kStep, a.mem_mode);
+          for (int it = 0; it < IT; ++it) v[j][it] = __builtin_nontemporal_load(gptr<V>(p + it * kStep));
         }
         if constexpr (BF) {
 #pragma unroll
@@ -475,7 +461,7 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
             if (jj < nj) {
               const uint64_t p = a.in[j0 + jj].base + s * a.in[j0 + jj].stride + off0;
 #pragma unroll
-              for (int it = 0; it < IT; ++it) v[jj][it] = get_mode<V>(p + it * kStep, a.mem_mode);
+              for (int it = 0; it < IT; ++it) v[jj][it] = __builtin_nontemporal_load(gptr<V>(p + it * kStep));
             }
           }
           if constexpr (BF) {
@@ -494,7 +480,7 @@ __device__ __forceinline__ void bytewise_tiles(const ApplyArgs &a) {
       for (int r = 0; r < R; ++r) {
         const uint64_t q = a.out[r].base + s * a.out[r].stride + off0;
 #pragma unroll
-        for (int it = 0; it < IT; ++it) put_mode<ACC, V>(q + it * kStep, acc[it][r], a.mem_mode);
+        for (int it = 0; it < IT; ++it) put_nt<ACC, V>(q + it * kStep, acc[it][r]);
       }
     } else {
       // ragged last tile: C is a multiple of 8, so a 16-byte lane unit may be half full
@@ -599,7 +585,7 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
       const uint64_t p = a.in[j].base + s * a.in[j].stride + off;
       V e[8];
 #pragma unroll
-      for (int x = 0; x < 8; ++x) e[x] = get_mode<V>(p + x * P, a.mem_mode);
+      for (int x = 0; x < 8; ++x) e[x] = __builtin_nontemporal_load(gptr<V>(p + x * P));
       if constexpr (MG) ml_add<8, DW>(ml, e, static_cast<uint32_t>(j));
       uint32_t c[R];
       uint32_t cm = 0;  // bits used by any output: no doublings past the highest one
@@ -635,7 +621,7 @@ __global__ __launch_bounds__(kBlock) void k_gf8_bitsliced(ApplyArgs a) {
       for (int r = 0; r < R; ++r) {
         const uint64_t q = a.out[r].base + s * a.out[r].stride + off;
 #pragma unroll
-        for (int x = 0; x < 8; ++x) put_mode<ACC, V>(q + x * P, acc[r][x], a.mem_mode);
+        for (int x = 0; x < 8; ++x) put_nt<ACC, V>(q + x * P, acc[r][x]);
         if constexpr (MG) ml_add<8, DW>(ml, acc[r], static_cast<uint32_t>(K + r));
       }
     }

@@ -1105,13 +1105,10 @@ void lsec_test_set_stamps(void *dev_buf, unsigned n) {
   lsec::set_launch_stamps(static_cast<unsigned long long *>(dev_buf), n);
 }
 
-// Test hook, not in include/: the XCD tile phase on (1) or off (0) for the following launches
-// (lsec::tile_phase_on; LSEC_TILE_PHASE sets the start value), for A/B runs in one allocation.
-void lsec_test_set_tile_phase(int on) { lsec::set_tile_phase(on); }
-
-// Test hook, not in include/: the bytewise / bit-sliced kernels' memory-instruction mode (bit 0 plain
-// stores, bit 1 plain loads; 0 non-temporal, the default) for the following launches (A/B runs).
-void lsec_test_set_mem_mode(int mode) { lsec::set_mem_mode(mode); }
+// Test hook, not in include/: the XCD tile phase for the following launches, bit 0 the tile loops,
+// bit 1 the compiled networks (lsec::tile_phase_on; LSEC_TILE_PHASE sets the start value, 1), for
+// A/B runs in one allocation.
+void lsec_test_set_tile_phase(int mode) { lsec::set_tile_phase(mode); }
 
 
 // Self-test of the bitmatrix decode planner (test hook, not in include/; no GPU): for the

@@ -1343,7 +1343,8 @@ def test_staging_pool_keeps_at_most_two_large_device_halves(cuda):
 def test_xcd_tile_phase_is_bit_identical(cuda, method, k, m, C, n, w):
     """The XCD tile phase (lsec_test_set_tile_phase; ApplyArgs::tile_phase, the networks' Args::phase)
     only changes which tile a workgroup takes: encode and single-erasure decode write the same bytes
-    with it on and off, in the bytewise kernel's queue and static forms and in the compiled networks."""
+    with it on and off, in the bytewise kernel's queue and static forms and in the compiled networks
+    (mode 3 = both; the default, 1, has it on for the tile loops only)."""
     import torch
 
     lib = L.lib()
@@ -1354,7 +1355,7 @@ def test_xcd_tile_phase_is_bit_identical(cuda, method, k, m, C, n, w):
         d = torch.randint(0, 256, (n, k, C), dtype=torch.uint8, device=cuda, generator=g)
         outs = []
         try:
-            for phase in (0, 1, 0):
+            for phase in (0, 3, 1):
                 lib.lsec_test_set_tile_phase(phase)
                 par = torch.zeros((n, m, C), dtype=torch.uint8, device=cuda)
                 p.encode_dev(d, par)
@@ -1363,7 +1364,7 @@ def test_xcd_tile_phase_is_bit_identical(cuda, method, k, m, C, n, w):
                 torch.cuda.synchronize()
                 outs.append((par, rb))
         finally:
-            lib.lsec_test_set_tile_phase(0)
+            lib.lsec_test_set_tile_phase(1)  # the default
         for par, rb in outs[1:]:
             assert torch.equal(par, outs[0][0])
             assert torch.equal(rb[:, 0], d[:, 1])

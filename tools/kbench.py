@@ -134,8 +134,6 @@ def main():
                 E.set_kernel_variant(v[0], v[1])
                 if len(v) > 2:  # a third field: the XCD tile phase (lsec_test_set_tile_phase)
                     E.lib().lsec_test_set_tile_phase(v[2])
-                if len(v) > 3:  # a fourth: the memory-instruction mode (lsec_test_set_mem_mode)
-                    E.lib().lsec_test_set_mem_mode(v[3])
                 e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
                 plan.encode_dev(data, par)
                 e0.record(stream)
@@ -166,8 +164,7 @@ def main():
             print(f"{name:6s} N={N:5d} mix probe (XOR of k to m, no GF)  {tm:8.3f} ms {eb / tm / 1e6:7.1f} GB/s ({eb / tm / 8e9:5.1%})",
                   flush=True)
         E.set_kernel_variant(0, 0)
-        E.lib().lsec_test_set_tile_phase(0)
-        E.lib().lsec_test_set_mem_mode(0)
+        E.lib().lsec_test_set_tile_phase(1)  # the default
         if a.magic:
             mg = torch.zeros((N, 4), dtype=torch.uint8, device=dev)
             tm = []
