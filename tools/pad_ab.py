@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--data-gib", type=float, default=16.0)
+    ap.add_argument("--pad-on", default="both", choices=("both", "data", "parity"),
+                    help="pad only the data rows (the reads) or only the parity rows (the writes)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     pads = [int(x) for x in a.pads.split(",")]
@@ -46,8 +48,10 @@ def main():
         out = torch.empty((N, 1, C), dtype=torch.uint8, device=dev)
         views = {}
         for pad in pads:
-            d = fd[: N * k * (C + pad)].view(N, k, C + pad)[:, :, :C]
-            p = fp[: N * m * (C + pad)].view(N, m, C + pad)[:, :, :C]
+            pd = pad if a.pad_on in ("both", "data") else 0
+            pp = pad if a.pad_on in ("both", "parity") else 0
+            d = fd[: N * k * (C + pd)].view(N, k, C + pd)[:, :, :C]
+            p = fp[: N * m * (C + pp)].view(N, m, C + pp)[:, :, :C]
             views[pad] = (d, p)
         # the same data bytes under every pad: copy pad 0's chunks into each padded view
         d0 = views[pads[0]][0].clone()
@@ -77,7 +81,7 @@ def main():
         for pad in pads:
             te = sorted(times[pad][0])[len(times[pad][0]) // 2]
             td = sorted(times[pad][1])[len(times[pad][1]) // 2]
-            print(f"{name:8s} N={N:5d} pad={pad:8d}  encode {te:7.3f} ms ({eb / te / 8e9:5.1%})   "
+            print(f"{name:8s} N={N:5d} pad={pad:8d} ({a.pad_on})  encode {te:7.3f} ms ({eb / te / 8e9:5.1%})   "
                   f"decode {td:7.3f} ms ({db / td / 8e9:5.1%})", flush=True)
         del fd, fp, out, views, d0, ref
         torch.cuda.empty_cache()
