@@ -33,6 +33,8 @@ CONFIGS = {
     "cg164c8": (L.CAUCHY_GOOD, 16, 4, 8 << 20),
     "cg164c1": (L.CAUCHY_GOOD, 16, 4, 1 << 20),
     "rs84c4": (L.REED_SOL_VAN, 8, 4, 4 << 20),
+    "cg206c4": (L.CAUCHY_GOOD, 20, 6, 4 << 20),
+    "cg42c4": (L.CAUCHY_GOOD, 4, 2, 4 << 20),
     "rs83c8": (L.REED_SOL_VAN, 8, 3, 8 << 20),
     "rs164c8": (L.REED_SOL_VAN, 16, 4, 8 << 20),
     "rs63c8": (L.REED_SOL_VAN, 6, 3, 8 << 20),
