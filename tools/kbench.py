@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Kernel A/B bench (development tool): interleaved rounds of encode/decode per kernel variant.
 
-python tools/kbench.py [--stripes N] [--rounds R] [--configs rs63,cg104,cg63]
+python tools/kbench.py [--stripes N] [--rounds R] [--configs rs63,cg104,cg63,cg:K:M:C_KiB,...]
 Prints HBM GB/s (algorithmic bytes / launch time, HIP events on the launch stream).
 """
 import argparse
@@ -90,6 +90,9 @@ def main():
     dev = torch.device("cuda:0")
     variants = [tuple(int(x) for x in v.split(",")) for v in a.variants.split(";")]
     for name in a.configs.split(","):
+        if name not in CONFIGS:  # "rs:K:M:C_KiB" / "cg:K:M:C_KiB"
+            t, kk, mm, ck = name.split(":")
+            CONFIGS[name] = ({"rs": L.REED_SOL_VAN, "cg": L.CAUCHY_GOOD}[t], int(kk), int(mm), int(ck) << 10)
         meth, k, m, C = CONFIGS[name][:4]
         w = CONFIGS[name][4] if len(CONFIGS[name]) > 4 else -1
         N = max(8, int(a.data_gib * 2**30 / (k * C)))
@@ -152,12 +155,14 @@ def main():
                 for i, e in enumerate(lost):
                     want = data[:, e] if e < k else ref_par[:, e - k]
                     assert torch.equal(out[:, i], want), f"variant {v} decode mismatch (shard {e})"
+        E.set_kernel_variant(0, 0)
+        net = int(plan.jit())
         for v in variants:
             te = sorted(res[v][0])[len(res[v][0]) // 2]
             td = sorted(res[v][1])[len(res[v][1]) // 2]
             eb = (k + m) * C * N
             db = (k + len(lost)) * C * N
-            print(f"{name:6s} N={N:5d} variant={v} jit={int(plan.jit()) if v[:2] == (0, 0) else 0}  encode {te:8.3f} ms {eb / te / 1e6:7.1f} GB/s "
+            print(f"{name:6s} N={N:5d} variant={v} jit={net if v[:2] == (0, 0) else 0}  encode {te:8.3f} ms {eb / te / 1e6:7.1f} GB/s "
                   f"({eb / te / 8e9:5.1%})   decode {td:8.3f} ms {db / td / 1e6:7.1f} GB/s ({db / td / 8e9:5.1%})",
                   flush=True)
         if tmix:
