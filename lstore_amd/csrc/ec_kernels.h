@@ -238,7 +238,8 @@ void make_cell(uint8_t c, CoefCell &cell);
 hipError_t launch_bytewise(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
 // encode + stripe magic in one pass (a.magic_acc != nullptr; checksum order = inputs, outputs)
 hipError_t launch_bytewise_magic(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
-hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0);
+// dw_pref: dwords per lane (1, 2, 4; 0 = 1) unless an A/B variant is set (lsec_set_kernel_variant)
+hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t stream, int grid_blocks = 0, int dw_pref = 0);
 // generic GF(2) bitmatrix codes (liberation / blaum_roth / liber8tion, liberation.c; Cauchy at
 // w = 16 / 32): w in LSEC_BITMATRIX_W by a kernel per w, any other 2 <= w <= kMaxW by the
 // LDS-staged kernel; R <= 2 per launch

@@ -295,12 +295,14 @@ hipError_t launch_bytewise_magic(const ApplyArgs &a, hipStream_t st, int grid_bl
   return by_r(a.R, [&](auto r) { return dispatch_bytewise_magic<decltype(r)::value>(a, st, grid); });
 }
 
-hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid_blocks) {
+hipError_t launch_bitsliced(const ApplyArgs &a, hipStream_t st, int grid_blocks, int dw_pref) {
   if (a.K < 1 || a.K > kMaxK || a.R < 1 || a.R > 8 || a.packet <= 0 || a.packet % 4 != 0 ||
       a.size % (8LL * a.packet) != 0)
     return hipErrorInvalidValue;
   if (a.nstripes <= 0 || a.size == 0) return hipSuccess;
-  int dw = (g_bs_variant == 2 || g_bs_variant == 4) && !a.magic_acc && !a.accumulate ? g_bs_variant : 1;
+  // dwords per lane: the A/B variant when one is set, else the caller's preference (1, 2, 4), else 1
+  const int want = g_bs_variant != 0 ? g_bs_variant : dw_pref;
+  int dw = (want == 2 || want == 4) && !a.magic_acc && !a.accumulate ? want : 1;
   while (dw > 1 && a.packet % (4 * dw) != 0) dw >>= 1;
   const uint64_t col_bytes = a.size / 8;
   const uint64_t tile = kBlock * 4ull * dw;

@@ -571,6 +571,22 @@ int check_geometry(const lio_erasure_plan_t *p, long long block_size) {
   return 0;
 }
 
+// Cauchy at w = 8 (KBITSLICED): the generic bit-sliced kernel or the compiled packet network, by
+// shape.  Round 6 (profiles/r06_v13_cauchy8_kernels_ab.txt: every c5 shape at C = 1, 4, 8 MiB, one
+// allocation each, interleaved): since the bit-sliced kernel took the work-sharing tail (round 5)
+// and the XCD tile phase (round 6), neither of which the networks have, it beats the network on
+// every shape with R <= 4 by 0.3-2.5 % -- at 4 dwords per lane from K = 16, and from K = 10 at
+// chunks of 4 MiB and up; 1 dword otherwise -- while the network keeps (20+6) (R = 6; up to 3.8 %
+// ahead at 4 MiB).  0: the network (where one is compiled), else the bit-sliced kernel's dwords per
+// lane.  lsec_test_set_cauchy8_policy(1) gives the network every shape it has one for (tests).
+std::atomic<int> g_c8_policy{0};
+
+int cauchy8_bitsliced_dw(int K, int R, long long size) {
+  if (g_c8_policy.load(std::memory_order_relaxed) == 1 || R > 4) return 0;
+  if (K >= 16 || (K >= 10 && size >= (4LL << 20))) return 4;
+  return 1;
+}
+
 // Enqueue out[r] = rows[r] . in  for every stripe, splitting R into launches of <= 8 rows
 // (<= 2 for the bitmatrix kernel) and K into groups of <= lsec::kMaxK inputs.  `image` is the
 // CoefCell[R][K] matrix image, the uint32 row masks [((r*w+l)*K + j)*NW + q] (KBITMATRIX) or the
@@ -603,7 +619,9 @@ int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in,
       size -= whole;
     }
   }
-  if ((kind == KBITMATRIX || kind == KBITSLICEDW || kind == KBITSLICED) && lsec::bitsliced_variant() == 0 &&
+  // Cauchy w = 8: the shape's kernel (cauchy8_bitsliced_dw; 0 = the network)
+  const int c8_dw = kind == KBITSLICED && w == 8 && lsec::bitsliced_variant() == 0 ? cauchy8_bitsliced_dw(K, R, size) : 0;
+  if ((kind == KBITMATRIX || kind == KBITSLICEDW || kind == KBITSLICED) && lsec::bitsliced_variant() == 0 && c8_dw == 0 &&
       lsec::jit::wants_pktnet(R, K, w) &&
       lsec::jit::pkt_aligned(in, K, out, R, w, packet))
     if (hipFunction_t fn = lsec::jit::ready(image, R, K)) {  // the bitmatrix's compiled packet network
@@ -646,7 +664,7 @@ int enqueue_apply(int kind, const void *image, int K, int R, const ShardRef *in,
                                : kind == KBITMATRIX ? lsec::launch_bitmatrix(b, st)
                                : kind == KWORDWISE  ? lsec::launch_wordwise(b, st)
                                : kind == KBITSLICEDW ? lsec::launch_gfw_bitsliced(b, st)
-                                                    : lsec::launch_bitsliced(b, st);
+                                                    : lsec::launch_bitsliced(b, st, 0, c8_dw);
         if (err != hipSuccess) return fail("kernel launch failed: %s", hipGetErrorString(err));
       }
     }
@@ -1086,6 +1104,8 @@ int lsec_plan_jit(lio_erasure_plan_t *plan, const int *erasures) {
     if (parse_erasures(plan, erasures, ids) != 0 || decode_entry(e, ids, &ent, &cells)) return 0;
     R = static_cast<int>(ent->dp.erased.size());
   }
+  // Cauchy w = 8 shapes the bit-sliced kernel serves (at the plan's chunk size) run no network
+  if (kind == KBITSLICED && plan->w == 8 && cauchy8_bitsliced_dw(plan->data_strips, R, plan->strip_size) > 0) return 0;
   return lsec::jit::ready(cells, R, plan->data_strips) != nullptr ? 1 : 0;
 }
 
@@ -1104,6 +1124,10 @@ int lsec_tile_sharing(void) { return lsec::tile_mode(); }
 void lsec_test_set_stamps(void *dev_buf, unsigned n) {
   lsec::set_launch_stamps(static_cast<unsigned long long *>(dev_buf), n);
 }
+
+// Test hook, not in include/: 1 = Cauchy at w = 8 on its compiled packet network wherever one exists,
+// 0 = by shape (cauchy8_bitsliced_dw, the default).
+void lsec_test_set_cauchy8_policy(int mode) { g_c8_policy.store(mode == 1 ? 1 : 0, std::memory_order_relaxed); }
 
 // Test hook, not in include/: the XCD tile phase for the following launches, bit 0 the tile loops,
 // bit 1 the compiled networks (lsec::tile_phase_on; LSEC_TILE_PHASE sets the start value, 1), for

@@ -127,24 +127,67 @@ def test_bitmatrix_network_vs_reference(cuda, method, k, w, P, nsuper):
     rp = O.RefPlan(method, k, m, w, P)
     want = np.stack([rp.encode(data[s]) for s in range(n)])
     losses = ([0], [k - 1], [k], [k + 1], [0, k - 1], [1, k], [k, k + 1]) + (([0, 2, k + 1, k + 3], [1, 3, 4]) if m >= 4 else ())
-    with L.Plan.new(method, size, k, m, w, P, 8) as p:
-        assert p.form_encoding_matrix() == 0 and p.form_decoding_matrix() == 0
+    # Cauchy at w = 8 with R <= 4 runs on the bit-sliced kernel by default (cauchy8_bitsliced_dw):
+    # the hook puts every shape on its network, so the networks stay tested
+    lib = L.lib()
+    lib.lsec_test_set_cauchy8_policy(1)
+    try:
+        with L.Plan.new(method, size, k, m, w, P, 8) as p:
+            assert p.form_encoding_matrix() == 0 and p.form_decoding_matrix() == 0
+            p.prepare_encode()
+            assert p.jit() == 1, "packet network not compiled"
+            par = torch.full((n, m, size), 0x5A, dtype=torch.uint8, device="cuda")
+            p.encode_dev(torch.from_numpy(data.copy()).cuda(), par)
+            assert np.array_equal(par.cpu().numpy(), want)
+            host = np.concatenate([data, np.zeros((n, m, size), np.uint8)], axis=1)
+            p.encode_stripes(host)
+            assert np.array_equal(host[:, k:], want)
+            for er in losses:
+                p.prepare_decode(er)
+                if len(er) >= 2 and er[0] < k and method in (L.LIBERATION, L.BLAUM_ROTH, L.LIBER8TION):
+                    assert p.jit(er) == 1, er  # two outputs on a network (single erasures: k_bitmatrix)
+                sh = host.copy()
+                sh[:, er] = 0x33
+                p.decode_stripes(sh, er)
+                assert_same(sh, host)
+    finally:
+        lib.lsec_test_set_cauchy8_policy(0)
+
+
+@pytest.mark.parametrize("method,k,m,C,net", [
+    (L.CAUCHY_GOOD, 10, 4, 4 << 20, False),   # c4: the bit-sliced kernel, 4 dwords per lane
+    (L.CAUCHY_GOOD, 4, 2, 1 << 20, False),    # 1 dword per lane
+    (L.CAUCHY_GOOD, 16, 4, 1 << 20, False),   # 4 dwords per lane from K = 16
+    (L.CAUCHY_GOOD, 20, 6, 1 << 20, True),    # R = 6: the packet network
+])
+def test_cauchy8_kernel_by_shape(cuda, method, k, m, C, net):
+    """Cauchy at w = 8 runs on the generic bit-sliced kernel for R <= 4 and on its compiled packet
+    network beyond (cauchy8_bitsliced_dw, ec_plan.cpp; profiles/r06_v13_cauchy8_kernels_ab.txt):
+    lsec_plan_jit says which, and the encode and a double-erasure decode are bit-exact against the
+    reference either way, device-resident."""
+    import torch
+
+    if not O.ref_available():
+        pytest.skip("oracle/_ref not built")
+    n = 3
+    with L.Plan.for_chunk(method, k, m, C) as p:
         p.prepare_encode()
-        assert p.jit() == 1, "packet network not compiled"
-        par = torch.full((n, m, size), 0x5A, dtype=torch.uint8, device="cuda")
-        p.encode_dev(torch.from_numpy(data.copy()).cuda(), par)
+        assert p.jit() == int(net), (k, m, C)
+        rng = np.random.default_rng(k + C)
+        data = rng.integers(0, 256, (n, k, C), dtype=np.uint8)
+        rp = O.RefPlan(method, k, m, 8, p.packet_size)
+        want = np.stack([rp.encode(data[s]) for s in range(n)])
+        rp.close()
+        d = torch.from_numpy(data).cuda()
+        par = torch.full((n, m, C), 0x5A, dtype=torch.uint8, device="cuda")
+        p.encode_dev(d, par)
         assert np.array_equal(par.cpu().numpy(), want)
-        host = np.concatenate([data, np.zeros((n, m, size), np.uint8)], axis=1)
-        p.encode_stripes(host)
-        assert np.array_equal(host[:, k:], want)
-        for er in losses:
-            p.prepare_decode(er)
-            if len(er) >= 2 and er[0] < k and method in (L.LIBERATION, L.BLAUM_ROTH, L.LIBER8TION):
-                assert p.jit(er) == 1, er  # two outputs on a network (single erasures: k_bitmatrix)
-            sh = host.copy()
-            sh[:, er] = 0x33
-            p.decode_stripes(sh, er)
-            assert_same(sh, host)
+        lost = [1, k]
+        p.prepare_decode(lost)
+        out = torch.zeros((n, 2, C), dtype=torch.uint8, device="cuda")
+        p.decode_dev(d, par, lost, out=out)
+        torch.cuda.synchronize()
+        assert torch.equal(out[:, 0], d[:, 1]) and torch.equal(out[:, 1], par[:, 0])
 
 
 @pytest.mark.parametrize("k", [128, 252])
