@@ -226,8 +226,9 @@ int lsec_prepare_decode(lio_erasure_plan_t *plan, const int *erasures);
  * kernel serves.  0 / -1. */
 int lsec_prepare_encode(lio_erasure_plan_t *plan);
 /* 1 when the encode (erasures == NULL) or the decode of that erasure pattern runs on a
- * compiled XOR network on the current device (wide GF(2^8) RS codes; RS / r6 at w = 16 / 32),
- * 0 otherwise. */
+ * compiled network on the current device (wide GF(2^8) RS codes; RS / r6 at w = 16 / 32; the
+ * packet networks of the liberation family and of Cauchy at w = 16 / 32, and at w = 8 with more
+ * than four outputs -- at the plan's strip_size), 0 otherwise. */
 int lsec_plan_jit(lio_erasure_plan_t *plan, const int *erasures);
 
 /* Devices that serve host-memory calls (et_*_stripes, et_*_magic, the plan's fn-pointers,
