@@ -667,6 +667,25 @@ hipError_t issue_runs(const std::vector<DmaRun> &v, hipMemcpyKind kind, hipStrea
 // run is period 1, rows 1.  Returns the number of groups, or -1 when out_cap is too small.
 // include/lstore_ec.h: wait until every in-place registration a call left to the background
 // unpinner is dropped (before the caller registers host memory with HIP itself)
+// Test hook, not part of include/*.h: the in-place stall guard without a GPU.  op 0: reset (no
+// suspension, empty window); op 1: report one pinned call's drain (bytes, drain_ms); op 2: 1 while
+// pinning in place is suspended, else 0.
+extern "C" int lsec_test_inplace_guard(int op, unsigned long long bytes, double drain_ms) {
+  using namespace lsec::eng;
+  if (op == 0) {
+    g_guard_calls.store(0);
+    g_guard_stalls.store(0);
+    g_guard_level.store(0);
+    g_guard_until_ns.store(0);
+    return 0;
+  }
+  if (op == 1) {
+    note_inplace_drain(static_cast<size_t>(bytes), drain_ms);
+    return 0;
+  }
+  return inplace_suspended() ? 1 : 0;
+}
+
 extern "C" int lsec_host_unpin_drain(void) {
   if (lsec::eng::Unpinner *u = lsec::eng::g_unpinner.load(std::memory_order_acquire)) u->drain();
   return 0;
