@@ -509,7 +509,7 @@ void call_trace_end() {
         g_trace_lines->reserve(1 << 16);
         atexit(print_trace_lines);
       }
-      g_trace_lines->emplace_back(buf);
+      if (g_trace_lines->size() < (1u << 21)) g_trace_lines->emplace_back(buf);  // (~0.5 GB at most)
     } else {
       fprintf(stderr, "%s\n", buf);
     }
