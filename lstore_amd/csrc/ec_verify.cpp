@@ -194,6 +194,16 @@ int control_check(lio_erasure_plan_t *plan, Stage &S, int w0, int cnt, const std
     std::fill(out.slot_of.begin(), out.slot_of.end(), -1);
     for (size_t r = 0; r < er.size(); ++r) out.slot_of[er[r]] = static_cast<int>(r);
     if (er.empty()) return 0;
+    // raid4 leaves a lost parity alone (raid4.c:48).  In a check in place (the first check, the
+    // carried guess: eptr[b] = ptr[b], jerasure.c:226) the reference's buffer then still holds
+    // the staged chunk, so its rebuild slot starts as that chunk; in the combination search the
+    // buffer is a pwork leftover (:284), which the slot's own leftover stands for.
+    if (ip && plan->method == RAID4)
+      for (int b : bad)
+        if (b >= n - m &&
+            hipMemcpy2DAsync(S.slot(w0, out.slot_of[b]), S.m * S.C, S.chunk(w0, b), S.n * S.C, S.C, cnt,
+                             hipMemcpyDeviceToDevice, S.st) != hipSuccess)
+          return lsec::set_error("control check: cannot stage a raid4 parity chunk");
     std::vector<int> e(er);
     e.push_back(-1);
     std::vector<lsec_shard_t> sh = refs(S, w0, out.slot_of);
@@ -584,11 +594,7 @@ int lsec_segment_read(lio_erasure_plan_t *plan, char **dev, int nstripes, int ch
   std::vector<int> work;
   for (int s = 0; s < nstripes; ++s) {
     std::vector<const uint8_t *> keys(n);
-    bool read_error = false;
-    for (int j = 0; j < n; ++j) {
-      keys[j] = reinterpret_cast<const uint8_t *>(rec(s, j));
-      read_error |= !keys[j];
-    }
+    for (int j = 0; j < n; ++j) keys[j] = reinterpret_cast<const uint8_t *>(rec(s, j));
     q[s] = vote(n, keys);
     if (q[s].none) {
       st[s] = kLost;
@@ -604,8 +610,9 @@ int lsec_segment_read(lio_erasure_plan_t *plan, char **dev, int nstripes, int ch
       for (int j = 0; j < n && !nonzero; ++j) nonzero = !all_zero(rec(s, j) + 4, C);
       data_ok = nonzero ? 1 : 2;
     }
-    if (data_ok == 1) {
-      if (paranoid || read_error) work.push_back(s);
+    if (data_ok == 1) {  // every data device in the quorum: verified in paranoid mode only (:1440-1442),
+                         // also when a parity device is unreadable
+      if (paranoid) work.push_back(s);
     } else if (data_ok == 2) {
       st[s] = kBlank;
     } else if (q[s].count < k) {

@@ -205,3 +205,81 @@ def test_legacy_inspect_with_more_controls_than_one_compare_launch(cuda, fix):
     if fix:
         sel = rw.astype(bool)
         assert np.array_equal(ours[sel], ref[sel])
+
+
+# The other codes of the plan API through the same read / inspect paths (raid4 has one parity
+# chunk, r6 its own encode, the bitmatrix codes packets): (method, k, m, C, w, packet)
+OTHER_CODES = [(L.RAID4, 6, 1, 4096, 8, 0), (L.REED_SOL_R6_OP, 6, 2, 4096, 8, 0), (L.CAUCHY_ORIG, 6, 3, 8192, 8, 0),
+               (L.LIBERATION, 6, 2, 7 * 32 * 8, 7, 32), (L.BLAUM_ROTH, 6, 2, 6 * 24 * 8, 6, 24),
+               (L.LIBER8TION, 6, 2, 8 * 32 * 8, 8, 32)]
+
+
+def other_plan(method, k, m, C, w, packet):
+    if packet:
+        p = L.Plan.new(method, C, k, m, w, packet)
+        p.form_encoding_matrix()
+        p.form_decoding_matrix()
+        return p
+    return L.Plan.for_chunk(method, k, m, C)
+
+
+@pytest.mark.gpu
+@needs_ref
+@pytest.mark.parametrize("method,k,m,C,w,packet", OTHER_CODES)
+@pytest.mark.parametrize("legacy", [False, True])
+def test_other_codes_read_and_inspect_match_reference(cuda, method, k, m, C, w, packet, legacy):
+    n, nstr, shift = k + m, 36, 1
+    data = np.stack([stripe(k, C, s + 31) for s in range(nstr)])
+    with other_plan(method, k, m, C, w, packet) as p:
+        rp = O.RefPlan(method, k, m, p.w, p.packet_size)
+        img = p.segment_write(data, shift, 0)
+        assert np.array_equal(img, rp.segment_write(data, nstr, C, shift, 0))
+        buf = logical_records(img, nstr, C, n)
+        kinds = damage(buf, k, m, np.random.default_rng(k + m + 5 * legacy), legacy)
+        ours, ref = buf.copy(), buf.copy()
+        st, bm, rw, state = p.segment_inspect(ours, C, fix=True, legacy_magic=legacy)
+        rst, rbm, rrw, cnt, brute = rp.segment_inspect(ref, nstr, C, 0 if legacy else 1, 1)
+        for s in range(nstr):
+            assert st[s] == rst[s], (s, kinds[s], st[s], rst[s])
+            assert np.array_equal(bm[s], rbm[s]), (s, kinds[s], bm[s], rbm[s])
+        assert np.array_equal(rw, rrw)
+        sel = rw.astype(bool)
+        assert np.array_equal(ours[sel], ref[sel])
+        dimg = np.zeros_like(img)
+        lc = C + 4
+        for s in range(nstr):
+            for j in range(n):
+                dimg[(j - s * shift) % n, s * lc:(s + 1) * lc] = buf[s, j]
+        for paranoid in (False, True):
+            out, rst_, bad = p.segment_read(dimg, nstr, C, shift, 0, paranoid=paranoid, legacy_magic=legacy)
+            rout, rrst, rbad = rp.segment_read(dimg, nstr, C, shift, 0, int(paranoid), 0 if legacy else 1)
+            assert bad == rbad and rst_.tolist() == rrst.tolist(), (paranoid, rst_.tolist(), rrst.tolist())
+            for s in range(nstr):
+                if rst_[s] >= 0:
+                    assert np.array_equal(out[s], rout[s]), (s, kinds[s])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,k,m,C,w,packet", OTHER_CODES + [(L.REED_SOL_VAN, 6, 3, 4096, 8, 0)])
+@pytest.mark.parametrize("missing", [0, 1])
+def test_read_with_a_device_missing_rebuilds_every_stripe(cuda, method, k, m, C, w, packet, missing):
+    """One device unreadable (NULL image); under the LUN rotation it holds a data chunk of some
+    stripes and a parity chunk of others.  A stripe whose data devices all agree is returned as
+    read (segment/jerasure.c:1416-1442); one missing a data device is rebuilt and verified.  In
+    paranoid mode every stripe is verified, and raid4, whose decode leaves a lost parity alone
+    (raid4.c:48), cannot verify a stripe without its parity: those stripes are unrecoverable, as
+    in the reference, and their data is left out."""
+    n, nstr = k + m, 2 * (k + m)
+    data = np.stack([stripe(k, C, s + 5) for s in range(nstr)])
+    held = [(missing + s) % n for s in range(nstr)]  # the logical chunk the missing device holds
+    parity_lost = [s for s in range(nstr) if held[s] >= k]
+    with other_plan(method, k, m, C, w, packet) as p:
+        img = p.segment_write(data, 1, 0)
+        for paranoid in (False, True):
+            out, st, bad = p.segment_read(img, nstr, C, 1, 0, paranoid=paranoid, missing=(missing,))
+            lost = parity_lost if paranoid and method == L.RAID4 else []
+            assert bad == len(lost) and [s for s in range(nstr) if st[s] < 0] == lost, (paranoid, st.tolist())
+            for s in range(nstr):
+                assert st[s] == (-1 if s in lost else 1 if held[s] < k else 0), (s, st[s])
+                if s not in lost:
+                    assert np.array_equal(out[s], data[s]), s
