@@ -64,14 +64,13 @@ void stream_copy(char *dst, const char *src, size_t n) {
   if (n) std::memcpy(dst, src, n);
 }
 
-// LSEC_NT_COPY=0: plain memcpy instead of streaming stores for the host copies (A/B runs)
-bool nt_copies() {
-  static const bool on = [] {
-    const char *v = getenv("LSEC_NT_COPY");
-    return !v || *v != '0';
-  }();
-  return on;
-}
+// LSEC_NT_COPY=0: plain memcpy instead of streaming stores for the host copies (A/B runs).  Read
+// once when the library loads, before any copy thread exists.
+const bool g_nt_copies = [] {
+  const char *v = getenv("LSEC_NT_COPY");
+  return !v || *v != '0';
+}();
+bool nt_copies() { return g_nt_copies; }
 
 void host_copy(char *dst, const char *src, size_t n) {
   if (nt_copies()) stream_copy(dst, src, n);
