@@ -24,6 +24,7 @@
 #include <string.h>
 #include <sys/uio.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "lstore_ec.h"
 
@@ -290,6 +291,91 @@ static void segment_round_trip(lio_erasure_plan_t *p, int N) {
   free(rewrite);
 }
 
+/* the scatter-list writes (segjerase_write_func's tbuf, :1786-1858): pieces cut at odd offsets,
+   equal to the contiguous write; the hand-off form's parity and magics equal the images' records */
+static void scatter_writes(lio_erasure_plan_t *p, int N) {
+  const int k = p->data_strips, m = p->parity_strips, n = k + m;
+  const int C = (int)p->strip_size;
+  const size_t rec = (size_t)C + 4, total = (size_t)N * k * C;
+  char *data = malloc(total);
+  fill(data, total, 11);
+  char **dev = malloc(sizeof(char *) * n), **dev2 = malloc(sizeof(char *) * n);
+  for (int i = 0; i < n; ++i) {
+    dev[i] = calloc(N, rec);
+    dev2[i] = calloc(N, rec);
+  }
+  CHECK(lsec_segment_write(p, data, N, C, 0, 0, dev) == 0, "segment_write for the scatter check");
+  struct iovec iov[8];
+  const size_t cut[8] = {0, 1, (size_t)C - 3, (size_t)C * k + 5, (size_t)C * k + 4096, total / 2 + 7, total - 9, total};
+  int niov = 0;
+  for (int i = 0; i + 1 < 8; ++i)
+    if (cut[i + 1] > cut[i]) iov[niov++] = (struct iovec){data + cut[i], cut[i + 1] - cut[i]};
+  CHECK(lsec_segment_write_iov(p, iov, niov, N, C, 0, 0, dev2) == 0, "segment_write_iov");
+  int same = 1;
+  for (int i = 0; i < n; ++i) same &= memcmp(dev[i], dev2[i], (size_t)N * rec) == 0;
+  CHECK(same, "%s(%d+%d): scatter write equals the contiguous write", JE_method[p->method], k, m);
+  const long long sb = lsec_segment_straddle_bytes(p, iov, niov, N, C);
+  char *parity = malloc((size_t)N * m * C), *magic = malloc(4 * (size_t)N), *straddle = malloc(sb > 0 ? sb : 1);
+  struct iovec *out = malloc(sizeof(struct iovec) * 2 * n * N);
+  const int got = lsec_segment_encode_iov(p, iov, niov, N, C, parity, magic, straddle, sb, out, 2 * n * N);
+  CHECK(got == 2 * n * N, "segment_encode_iov returned %d", got);
+  int ok = got == 2 * n * N;
+  for (int s = 0; ok && s < N; ++s) {
+    ok &= memcmp(magic + 4 * s, dev[0] + s * rec, 4) == 0;
+    for (int r = 0; r < m; ++r) ok &= memcmp(parity + ((size_t)s * m + r) * C, dev[k + r] + s * rec + 4, C) == 0;
+    for (int j = 0; j < n; ++j) /* [magic | chunk] iovecs in logical order */
+      ok &= out[2 * (s * n + j)].iov_len == 4 && out[2 * (s * n + j) + 1].iov_len == (size_t)C &&
+            memcmp(out[2 * (s * n + j) + 1].iov_base, dev[j] + s * rec + 4, C) == 0;
+  }
+  CHECK(ok, "%s(%d+%d): hand-off parity, magics and iovecs", JE_method[p->method], k, m);
+  for (int i = 0; i < n; ++i) {
+    free(dev[i]);
+    free(dev2[i]);
+  }
+  free(dev);
+  free(dev2);
+  free(data);
+  free(parity);
+  free(magic);
+  free(straddle);
+  free(out);
+}
+
+/* et_encode / et_decode over files (erasure_tools.c:339-600) */
+static void file_tools(lio_erasure_plan_t *p) {
+  const int k = p->data_strips, m = p->parity_strips;
+  const long long strip = p->strip_size, fsize = k * strip - 13, foff = 100, poff = 7;
+  const char *tmp = getenv("TMPDIR") ? getenv("TMPDIR") : "/tmp";
+  char dname[512], pname[512];
+  snprintf(dname, sizeof dname, "%s/host_san_%d.data", tmp, (int)getpid());
+  snprintf(pname, sizeof pname, "%s/host_san_%d.parity", tmp, (int)getpid());
+  char *buf = malloc(foff + k * strip);
+  memset(buf, '0', foff + k * strip);
+  fill(buf + foff, fsize, 5);
+  FILE *f = fopen(dname, "w");
+  CHECK(f && fwrite(buf, 1, foff + fsize, f) == (size_t)(foff + fsize), "write %s", dname);
+  if (f) fclose(f);
+  remove(pname);
+  CHECK(et_encode(p, dname, foff, pname, poff, 1 << 20) == 0, "et_encode");
+  f = fopen(dname, "r+");
+  if (f) { /* lose data strip 1 */
+    fseek(f, foff + strip, SEEK_SET);
+    for (long long i = 0; i < strip; ++i) fputc(0xEE, f);
+    fclose(f);
+  }
+  int er[3] = {1, m > 1 ? k : -1, -1};
+  CHECK(et_decode(p, foff + fsize, dname, foff, pname, poff, 1 << 20, er) == 0, "et_decode");
+  char *back = malloc(foff + fsize);
+  f = fopen(dname, "r");
+  CHECK(f && fread(back, 1, foff + fsize, f) == (size_t)(foff + fsize), "read back");
+  if (f) fclose(f);
+  CHECK(memcmp(back + foff, buf + foff, fsize) == 0, "%s(%d+%d): file tools round trip", JE_method[p->method], k, m);
+  remove(dname);
+  remove(pname);
+  free(buf);
+  free(back);
+}
+
 static double now_s(void) {
   struct timespec t;
   clock_gettime(CLOCK_MONOTONIC, &t);
@@ -327,7 +413,11 @@ static void gpu_part(int threads, int iters) {
       calls += wk[t].calls;
     }
     stripes += batched(p, f->C >= (1 << 20) ? 8 : 64);
-    if (f->k + f->m <= 32 && f->C <= (1 << 20)) segment_round_trip(p, 9);
+    if (f->k + f->m <= 32 && f->C <= (1 << 20)) {
+      segment_round_trip(p, 9);
+      scatter_writes(p, 5);
+    }
+    if (f->C <= (1 << 20)) file_tools(p);
     et_destroy_plan(p);
   }
   printf("{\"part\": \"gpu\", \"threads\": %d, \"per_stripe_calls\": %lld, \"batched_stripes\": %lld, "
