@@ -389,6 +389,8 @@ static void gpu_part(int threads, int iters) {
       {LIBERATION, 6, 2, 7, 7 * 32 * 64, 32}, {BLAUM_ROTH, 6, 2, 6, 6 * 24 * 64, 24}, {LIBER8TION, 6, 2, -1, 65536},
       {CAUCHY_ORIG, 8, 4, -1, 65536},
       {REED_SOL_VAN, 10, 4, 16, 262144}, {CAUCHY_GOOD, 20, 6, -1, 262144}, {REED_SOL_VAN, 6, 3, -1, 4 << 20},
+      {REED_SOL_VAN, 20, 6, -1, 262144}, /* a compiled w = 8 network once it is ready */
+      {REED_SOL_VAN, 10, 4, 32, 262144}, {CAUCHY_GOOD, 10, 4, 16, 262144},
   };
   long long calls = 0, stripes = 0;
   const double t0 = now_s();
@@ -400,6 +402,7 @@ static void gpu_part(int threads, int iters) {
     if (!p) continue;
     p->form_encoding_matrix(p);
     p->form_decoding_matrix(p);
+    CHECK(lsec_prepare_encode(p) == 0, "prepare_encode"); /* waits for a compiled network where one is made */
     pthread_t th[64];
     worker_t wk[64];
     const int T = threads < 64 ? threads : 64;
@@ -418,6 +421,22 @@ static void gpu_part(int threads, int iters) {
       scatter_writes(p, 5);
     }
     if (f->C <= (1 << 20)) file_tools(p);
+    et_destroy_plan(p);
+  }
+  { /* one batched shape through every tile-dealing mode and a two-entry host device set */
+    lio_erasure_plan_t *p = et_generate_plan(6ll << 20, REED_SOL_VAN, 6, 3, -1, -1, -1);
+    p->form_encoding_matrix(p);
+    p->form_decoding_matrix(p);
+    const int mode0 = lsec_tile_sharing();
+    for (int mode = 0; mode < 3; ++mode) {
+      lsec_set_tile_sharing(mode);
+      stripes += batched(p, 24);
+    }
+    lsec_set_tile_sharing(mode0);
+    const int devs[2] = {0, 0};
+    CHECK(lsec_set_host_devices(devs, 2) == 0, "host device set");
+    stripes += batched(p, 48);
+    CHECK(lsec_set_host_devices(NULL, 0) == 0, "host device set cleared");
     et_destroy_plan(p);
   }
   printf("{\"part\": \"gpu\", \"threads\": %d, \"per_stripe_calls\": %lld, \"batched_stripes\": %lld, "
