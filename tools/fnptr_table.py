@@ -24,15 +24,17 @@ def main():
         for line in open(path):
             r = json.loads(line)
             key = (r["op"], r["method"], r["chunk"], r["threads"])
+            fa = r.get("free_after", 0)  # the harness's buffer lifetime: compared like with like
             if r["impl"] == "reference":
-                ref[key].append(r)
+                ref[key + (fa,)].append(r)
             else:
                 env = r.get("env", "").strip()
-                eng[key + (("page-locked " if r["pinned"] else "") + env,)].append(r)
+                eng[key + (("page-locked " if r["pinned"] else "") + env, fa)].append(r)
     print("| op | method | C | threads | engine run | reference GiB/s (p50 / p99 us) | engine GiB/s (p50 / p99 us) | engine / reference |")
     print("|---|---|---|---|---|---|---|---|")
     for key in sorted(eng, key=lambda k: (k[0], k[1], k[2], k[3], k[4])):
-        rc, rv = cell(ref[key[:4]]) if ref.get(key[:4]) else ("-", None)
+        rk = key[:4] + (key[5],)
+        rc, rv = cell(ref[rk]) if ref.get(rk) else ("-", None)
         ec, ev = cell(eng[key])
         ratio = f"{ev / rv:.2f}" if rv else "-"
         print(f"| {key[0]} | {key[1]} | {key[2] >> 10} KiB | {key[3]} | {key[4] or 'default'} | {rc} | {ec} | {ratio} |")

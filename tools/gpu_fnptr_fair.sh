@@ -14,7 +14,11 @@ cases=${*:-"1048576:1:cauchy_good:decode 1048576:8:cauchy_good:decode 65536:8:ca
 for c in $cases; do
   IFS=: read -r chunk threads method op envs <<< "$c"
   for impl in engine reference; do
-    if [ $impl = reference ]; then extra="FNPTR_ONLY_REF=1"; else extra="${envs//,/ }"; fi
+    # the harness's own settings (FNPTR_*: buffer lifetime, page-locked buffers) apply to both
+    # sides, the engine's (LSEC_*) to the engine only
+    harness=""
+    for e in ${envs//,/ }; do case $e in FNPTR_*) harness="$harness $e" ;; esac; done
+    if [ $impl = reference ]; then extra="FNPTR_ONLY_REF=1$harness"; else extra="${envs//,/ }"; fi
     env FNPTR_REF=oracle/_ref/libjerasure_ref.so $extra timeout -k 10 60 build/fnptr_bench "$chunk" "$threads" 2 "$method" "$op" \
       | sed "s/}\$/, \"env\": \"$extra\"}/" >> "$out" || { echo "failed: $c $impl"; exit 1; }
   done
