@@ -13,6 +13,7 @@ import pytest
 import lstore_amd as L
 import oracle as O
 from patterns import stripe
+from test_verify import OTHER_CODES, other_plan
 
 
 def py_segment_images(method, data, m, chunk, n_shift, first, packet=0):
@@ -248,3 +249,17 @@ def test_segment_encode_iov_is_the_reference_hand_off(cuda, method, k, m, chunk)
                 assert iovs[2 * (s * (k + m) + j) + 1][0] == base + (s * k + j) * chunk
         with pytest.raises(L.ErasureError, match="bytes in the scatter list"):
             p.segment_encode_iov([flat[:-8]], N, chunk)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,k,m,C,w,packet", OTHER_CODES)
+def test_other_codes_scatter_write_matches_reference(cuda, method, k, m, C, w, packet):
+    """The scatter-list write for raid4, r6, Cauchy-orig and the bitmatrix codes: identical images."""
+    N = 6
+    data = np.stack([stripe(k, C, s + 19) for s in range(N)])
+    with other_plan(method, k, m, C, w, packet) as p:
+        rp = O.RefPlan(method, k, m, p.w, p.packet_size)
+        for fracs, errs in SCATTER_CASES:
+            pieces = scatter(data, _cut_points(k, C, fracs), errs)
+            assert np.array_equal(p.segment_write_iov(pieces, N, C, 2, 5), rp.segment_write_iov(pieces, N, C, 2, 5)), \
+                (fracs, errs)
