@@ -90,9 +90,9 @@ struct ZcSlot {  // one calling thread's page-locked slot on one device
     }
     HIP_OK(hipHostMalloc(reinterpret_cast<void **>(&flag), 64, hipHostMallocCoherent));
     *flag = 0;
-    void *d = nullptr;
-    HIP_OK(hipHostGetDevicePointer(&d, flag, 0));
-    dflag = static_cast<unsigned *>(d);
+    void *dp = nullptr;
+    HIP_OK(hipHostGetDevicePointer(&dp, flag, 0));
+    dflag = static_cast<unsigned *>(dp);
     HIP_OK(hipMalloc(reinterpret_cast<void **>(&counter), 64));
     HIP_OK(hipMemset(counter, 0, 64));
     return 0;
