@@ -1,4 +1,4 @@
-"""world_size-2 gloo rehearsal of bench.py's multi-GPU path (CPU only).
+"""gloo rehearsal (2, 4 and 8 ranks) of bench.py's multi-GPU path (CPU only).
 
 The ranks run bench.py's own code: ``bench.launch`` self-spawns them (WORLD_SIZE unset,
 ``--gpus 2``) and each runs ``bench.run_rank`` -- partition, warm-up, the barrier-bracketed
@@ -132,25 +132,26 @@ def _args(*extra):
                         "--no-layout-ab", "--no-copy-ref", *extra])
 
 
-@pytest.mark.parametrize("total", [7, 16])
-def test_self_launched_two_ranks_match_single_process(built, tmp_path, monkeypatch, total):
-    """bench.launch(--gpus 2) with no external launcher: two gloo ranks, strong partition."""
+@pytest.mark.parametrize("world,total", [(2, 7), (2, 16), (4, 16), (8, 16), (8, 9)])
+def test_self_launched_ranks_match_single_process(built, tmp_path, monkeypatch, world, total):
+    """bench.launch(--gpus N) with no external launcher: N gloo ranks, strong partition (the
+    driver's 4- and 8-GPU runs rehearsed on the CPU)."""
     import oracle as O
     from patterns import stripe
 
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     monkeypatch.setenv("LSEC_TEST_DUMP", str(tmp_path))
     out = tmp_path / "line.json"
-    rc = bench.launch(_args("--gpus", "2", "--total-stripes", str(total), "--json-out", str(out)), OracleEngine)
+    rc = bench.launch(_args("--gpus", str(world), "--total-stripes", str(total), "--json-out", str(out)), OracleEngine)
     assert rc == 0
     line = json.loads(out.read_text())
-    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
-    assert [r["rank"] for r in line["per_rank"]] == [0, 1]
-    assert [r["stripes"] for r in line["per_rank"]] == [b - a for a, b in (stripe_range(total, 2, r) for r in range(2))]
+    assert line["n_gpus"] == world and line["scaling"] == "strong"
+    assert [r["rank"] for r in line["per_rank"]] == list(range(world))
+    assert [r["stripes"] for r in line["per_rank"]] == [b - a for a, b in (stripe_range(total, world, r) for r in range(world))]
     assert all(r["parity_ok"] for r in line["per_rank"])
     assert line["value"] > 0 and line["ms_per_step"] > 0
     merged = {}
-    for r in range(2):
+    for r in range(world):
         part = {int(s): c for s, c in json.loads((tmp_path / f"rank{r}.json").read_text()).items()}
         assert not set(part) & set(merged)
         merged.update(part)
@@ -159,20 +160,21 @@ def test_self_launched_two_ranks_match_single_process(built, tmp_path, monkeypat
         assert merged[s] == zlib.crc32(O.encode(O.REED_SOL_VAN, stripe(6, 4096, s), 3).tobytes())
 
 
-def test_self_launched_weak_scaling(built, tmp_path, monkeypatch):
+@pytest.mark.parametrize("world", [2, 8])
+def test_self_launched_weak_scaling(built, tmp_path, monkeypatch, world):
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     monkeypatch.setenv("LSEC_TEST_DUMP", str(tmp_path))
     out = tmp_path / "line.json"
-    rc = bench.launch(_args("--gpus", "2", "--stripes", "3", "--method", "cauchy_good", "--json-out", str(out)),
+    rc = bench.launch(_args("--gpus", str(world), "--stripes", "3", "--method", "cauchy_good", "--json-out", str(out)),
                       OracleEngine)
     assert rc == 0
     line = json.loads(out.read_text())
-    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
-    assert [r["stripes"] for r in line["per_rank"]] == [3, 3]
+    assert line["n_gpus"] == world and line["scaling"] == "weak"
+    assert [r["stripes"] for r in line["per_rank"]] == [3] * world
     seen = set()
-    for r in range(2):
+    for r in range(world):
         seen |= {int(s) for s in json.loads((tmp_path / f"rank{r}.json").read_text())}
-    assert seen == set(range(6))  # rank r owns stripes [3r, 3r+3)
+    assert seen == set(range(3 * world))  # rank r owns stripes [3r, 3r+3)
 
 
 def test_host_path_on_every_rank_with_aggregate(built, tmp_path, monkeypatch):
