@@ -377,6 +377,10 @@ extern std::atomic<unsigned long long> g_st_parks, g_st_spin_hits, g_st_claim_mi
 int server_run(int dev, PlanExt *e, char **ptrs, long long C, const std::vector<int> &in_ids,
                const std::vector<int> &out_ids, const void *image, int kind, const CallerPinned *cp);
 void servers_restart();  // stop every server (the next launch takes new test settings)
+// Around a hipHostUnregister (ec_pinning.cpp), which waits until the device is idle: running
+// stripe servers are stopped and none is launched until the matching end (ec_stripe_server.cpp)
+void servers_yield_begin();
+void servers_yield_end();
 extern std::atomic<int> g_srv_timeout_ms, g_srv_hold;
 extern std::atomic<unsigned long long> g_st_srv_timeouts;
 

@@ -374,11 +374,15 @@ bool InPlacePin::pin(char **ptrs, int nstripes, int km, const std::vector<int> &
 
 namespace {
 void unregister_all(const std::vector<char *> &held) {
+  if (held.empty()) return;
+  // hipHostUnregister waits for an idle device: running stripe servers step aside meanwhile
+  servers_yield_begin();
   for (char *b : held)
     if (quiet([&] { return hipHostUnregister(b); }) != hipSuccess) {
       static std::atomic<bool> told{false};
       if (!told.exchange(true)) fprintf(stderr, "liblstore_ec: hipHostUnregister(%p) failed\n", static_cast<void *>(b));
     }
+  servers_yield_end();
 }
 
 void unclaim(const std::vector<std::pair<uintptr_t, uintptr_t>> &claimed) {

@@ -34,6 +34,10 @@ namespace eng {
 std::atomic<int> g_srv_timeout_ms{5000};
 std::atomic<int> g_srv_hold{0};
 std::atomic<unsigned long long> g_st_srv_timeouts{0};
+// In-place releases running (servers_yield_begin / _end): no server launches meanwhile
+std::atomic<int> g_srv_yield{0};
+std::atomic<unsigned long long> g_st_srv_yields{0};
+std::mutex g_registry_mu;  // the registry of servers (creation, and the walks of stop_all / yield)
 
 class StripeServer {
  public:
@@ -42,9 +46,8 @@ class StripeServer {
     static std::atomic<StripeServer *> fast[64] = {};
     if (dev >= 0 && dev < 64)
       if (StripeServer *f = fast[dev].load(std::memory_order_acquire)) return f;
-    static std::mutex m;
     static std::map<int, StripeServer *> all;  // intentionally leaked: lives until exit
-    std::lock_guard<std::mutex> lk(m);
+    std::lock_guard<std::mutex> lk(g_registry_mu);
     StripeServer *&r = all[dev];
     if (!r) {
       r = new StripeServer(dev);
@@ -267,6 +270,7 @@ class StripeServer {
   }
   // at exit: stop every running server and let it drain (its stop word is read on every idle poll)
   static void stop_all() {
+    std::lock_guard<std::mutex> rk(g_registry_mu);
     for (StripeServer *s : registry()) {
       std::lock_guard<std::mutex> lk(s->mu_);
       if (s->sh_) s->stop_and_settle(0, nullptr, nullptr);
@@ -276,6 +280,27 @@ class StripeServer {
  public:
   // test hook (lsec_test_server_hold): stop every server, so the next launch takes the new hold
   static void restart_all() { stop_all(); }
+  // servers_yield_begin: stop the running launches.  No part is cancelled: what was posted and
+  // not yet served stays posted, and the next launch serves it (as after an idle retirement).
+  static void stop_running() {
+    std::lock_guard<std::mutex> rk(g_registry_mu);
+    for (StripeServer *s : registry()) {
+      if (!s->running_.load(std::memory_order_acquire)) continue;
+      std::lock_guard<std::mutex> lk(s->mu_);
+      if (s->sh_ && s->running_) {
+        s->stop_and_settle(0, nullptr, nullptr);
+        s->yield_stopped_.store(true, std::memory_order_release);
+        g_st_srv_yields.fetch_add(1, std::memory_order_relaxed);
+      }
+    }
+  }
+  // servers_yield_end, the last release done: relaunch the servers a release stopped, so calls
+  // posted meanwhile are served now rather than at their wait loop's next check
+  static void relaunch_yielded() {
+    std::lock_guard<std::mutex> rk(g_registry_mu);
+    for (StripeServer *s : registry())
+      if (s->yield_stopped_.exchange(false, std::memory_order_acq_rel)) (void)s->ensure_running(false);
+  }
 
  private:
   // Stop the running server and wait (bounded) until it has left.  The stop word is final (the
@@ -400,6 +425,10 @@ class StripeServer {
       }
     }
     if (running_) return 0;
+    // an in-place release is waiting for the device to go idle (servers_yield_begin): no launch
+    // until it is done; the posting caller's wait loop asks again within 500 us.  Checked under
+    // mu_, which the release's stop also takes, so a launch that got in first is stopped by it.
+    if (g_srv_yield.load(std::memory_order_acquire) > 0) return 0;
     for (int g = 0; g < lsec::kSrvWG; ++g) sh_->post[g][lsec::kSrvSlotsPerWG] = 0;  // stop word
     lsec::SrvArgs a;
     a.shared = reinterpret_cast<lsec::SrvShared *>(sh_dev_);
@@ -449,6 +478,7 @@ class StripeServer {
   static constexpr int kStopWaitS = 30;  // how long stop_and_settle waits for a launch to leave
   std::atomic<int64_t> last_seen_us_{0};
   std::atomic<int64_t> last_check_us_{0};
+  std::atomic<bool> yield_stopped_{false};  // stopped by a release (stop_running), to relaunch after it
 };
 
 int server_run(int dev, PlanExt *e, char **ptrs, long long C, const std::vector<int> &in_ids,
@@ -457,6 +487,19 @@ int server_run(int dev, PlanExt *e, char **ptrs, long long C, const std::vector<
 }
 
 void servers_restart() { StripeServer::restart_all(); }
+
+// hipHostUnregister waits until the device is idle, and a running stripe server never is while
+// per-stripe calls keep coming: beside one thread of back-to-back 16 KiB calls a 1 MiB call pinned
+// in place made no progress for 4 s (tools/probes/mixed_sizes_probe.c).  So a release stops the
+// running servers first and holds off launches until it is done; calls posted meanwhile are
+// served by the launch their wait loop makes after it (within 500 us).
+void servers_yield_begin() {
+  g_srv_yield.fetch_add(1, std::memory_order_acq_rel);
+  StripeServer::stop_running();
+}
+void servers_yield_end() {
+  if (g_srv_yield.fetch_sub(1, std::memory_order_acq_rel) == 1) StripeServer::relaunch_yielded();
+}
 
 }  // namespace eng
 }  // namespace lsec

@@ -513,3 +513,50 @@ def test_no_registration_outlives_its_call(cuda):
     assert st["calls"] == 144 and not st["bad"], st
     assert st["still_registered"] == 0, st
     assert st["copies_checked"] == 144 and st["reused_address"] > 0, st
+
+
+def test_large_calls_progress_beside_back_to_back_small_calls(cuda):
+    """An LStore process serving segments of different chunk sizes: two threads make back-to-back
+    16 KiB decodes (the stripe server stays resident) while a third makes 1 MiB decodes, which pin
+    their chunks in place and release them with hipHostUnregister -- a call that waits until the
+    device is idle.  The releases stop the server and hold off its relaunch while they run
+    (servers_yield_begin, ec_stripe_server.cpp); before that the 1 MiB calls made no progress at
+    all until the small calls stopped (tools/probes/mixed_sizes_probe.c).  Every output checked."""
+    k, m = 6, 3
+    stop = threading.Event()
+    errors, small_calls, large_lat = [], [0, 0], []
+
+    def worker(C, idx):
+        with L.Plan.for_chunk(L.CAUCHY_GOOD, k, m, C) as p:
+            rng = np.random.default_rng(C + idx)
+            sh = [rng.integers(0, 256, C, dtype=np.uint8) for _ in range(k)] + [np.zeros(C, np.uint8) for _ in range(m)]
+            p.encode_block(sh)
+            want = sh[0].copy()
+            while not stop.is_set():
+                sh[0][:] = 0xA5
+                t0 = time.perf_counter()
+                rc = p.decode_block(sh, [0])
+                dt = time.perf_counter() - t0
+                if rc != 0 or not np.array_equal(sh[0], want):
+                    errors.append((C, rc))
+                    return
+                if C > 65536:
+                    large_lat.append(dt)
+                else:
+                    small_calls[idx] += 1
+
+    th = [threading.Thread(target=worker, args=(16384, i)) for i in range(2)]
+    for t in th:
+        t.start()
+    time.sleep(0.3)  # the small calls run (and the server with them) before the large ones start
+    big = threading.Thread(target=worker, args=(1 << 20, 0))
+    big.start()
+    time.sleep(2.5)
+    stop.set()
+    for t in th + [big]:
+        t.join(timeout=60)
+    assert not errors, errors
+    assert sum(small_calls) > 1000, small_calls
+    # a 1 MiB decode alone takes ~0.2 ms; starved, not one finished before the small calls stopped
+    assert len(large_lat) >= 50, (len(large_lat), small_calls)
+    assert max(large_lat) < 1.0, max(large_lat)
