@@ -376,6 +376,57 @@ static void file_tools(lio_erasure_plan_t *p) {
   free(back);
 }
 
+/* small and large per-stripe calls side by side (the stripe server running while calls pinned in
+   place release their registrations: servers_yield_begin / _end) */
+typedef struct {
+  lio_erasure_plan_t *p;
+  double t_end;
+  long calls;
+} mixed_t;
+static double now_s(void);
+static void *mixed_worker(void *arg) {
+  mixed_t *w = arg;
+  lio_erasure_plan_t *p = w->p;
+  const int k = p->data_strips, m = p->parity_strips;
+  const size_t C = (size_t)p->strip_size;
+  char *buf = malloc((size_t)(k + m) * C), *keep = malloc(C);
+  char *ptr[32];
+  fill(buf, (size_t)k * C, C + 3);
+  for (int i = 0; i < k + m; ++i) ptr[i] = buf + (size_t)i * C;
+  p->encode_block(p, ptr, (int)C);
+  memcpy(keep, ptr[0], C);
+  int er[2] = {0, -1};
+  while (now_s() < w->t_end) {
+    memset(ptr[0], 0x5C, C);
+    const int rc = p->decode_block(p, ptr, (int)C, er);
+    CHECK(rc == 0 && memcmp(ptr[0], keep, C) == 0, "mixed sizes: C=%zu decode", C);
+    ++w->calls;
+  }
+  free(buf);
+  free(keep);
+  return NULL;
+}
+static void mixed_sizes(double secs) {
+  lio_erasure_plan_t *ps = et_generate_plan(6 * 16384, CAUCHY_GOOD, 6, 3, -1, -1, -1);
+  lio_erasure_plan_t *pl = et_generate_plan(6 << 20, CAUCHY_GOOD, 6, 3, -1, -1, -1);
+  ps->form_encoding_matrix(ps), ps->form_decoding_matrix(ps);
+  pl->form_encoding_matrix(pl), pl->form_decoding_matrix(pl);
+  mixed_t w[4];
+  pthread_t th[4];
+  const double t_end = now_s() + secs;
+  for (int i = 0; i < 4; ++i) {
+    w[i] = (mixed_t){i < 2 ? ps : pl, t_end, 0};
+    pthread_create(&th[i], NULL, mixed_worker, &w[i]);
+  }
+  for (int i = 0; i < 4; ++i) pthread_join(th[i], NULL);
+  CHECK(w[0].calls + w[1].calls > 100 && w[2].calls + w[3].calls > 10, "mixed sizes progress: %ld small, %ld large",
+        w[0].calls + w[1].calls, w[2].calls + w[3].calls);
+  printf("{\"part\": \"mixed sizes\", \"small_calls\": %ld, \"large_calls\": %ld}\n", w[0].calls + w[1].calls,
+         w[2].calls + w[3].calls);
+  et_destroy_plan(ps);
+  et_destroy_plan(pl);
+}
+
 static double now_s(void) {
   struct timespec t;
   clock_gettime(CLOCK_MONOTONIC, &t);
@@ -452,6 +503,7 @@ int main(int argc, char **argv) {
   fflush(stdout);
   if (lsec_device_count() > 0) {
     gpu_part(threads, iters);
+    mixed_sizes(3.0);
     lsec_host_unpin_drain();
   }
   return g_fails ? 1 : 0;
